@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""bench.py — frame-pair alignments/sec of the MI355X ImageAlignment path (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1] = SURVEY.md §8(d) config 2): sparse image alignment of KITTI-shaped
+frame pairs, 1241x376 grey, 2000 features (1000 on the ref frame + 1000 on its last keyframe), patch 5,
+5-level pyramid (levels 4..0), one Tukey-weighted LM step per level.  A "step" is one pass of the hot
+path over one batch: --pairs independent pairs per GPU (default 512), inputs (pyramids, features,
+poses) resident in HBM before the timed region.  Data: synthetic street scenes (svo_amd.synth, seeds
+0x5EED0000 + global pair index modulo --distinct), each pair in its own HBM buffers.
+
+Multi-GPU: one process per GPU (torch.distributed.run); pairs are independent, so each rank aligns its
+own --pairs (weak scaling) and there is no data-path collective: the gloo process group is used only
+for the barrier and the max-over-ranks time.
+
+Prints one JSON line (rank 0).  See DESIGN.md §Measurement for the roofline and baseline definitions.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import svo_amd  # noqa: E402  (loads libsvo_hip.so before torch can bring its own HIP runtime)
+import svo_amd.synth as synth  # noqa: E402
+
+METRIC = "frame-pair alignments/sec @2000 feats, 5-lvl pyramid; SE(3) err vs ref"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--pairs", type=int, default=512, help="frame pairs per GPU per step")
+    ap.add_argument("--features", type=int, default=2000)
+    ap.add_argument("--levels", type=int, default=5)
+    ap.add_argument("--patch", type=int, default=5)
+    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic scenes per rank")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the single-core CPU baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-core CPU baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc-json", default=None, help="rocprofv3 PMC summary (tools/pmc_traffic.py output)")
+    return ap.parse_args()
+
+
+def level_bytes(w, h, levels):
+    tot = 0
+    for _ in range(levels):
+        tot += w * h
+        w, h = (w + 1) // 2, (h + 1) // 2
+    return tot
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: E402  (gloo: host-side barrier / max only)
+        dist.init_process_group(backend="gloo")
+
+    ctx = svo_amd.Context(local_rank)
+    P, nf, L, patch = args.pairs, args.features, args.levels, args.patch
+    D = max(1, min(args.distinct, P))
+    nthreads = max(1, min(16, os.cpu_count() or 1))
+    scenes = [synth.make_pair(seed=synth.SEED_BASE + rank * P + i, n_features=nf, patch_size=patch, nthreads=nthreads)
+              for i in range(D)]
+    cam = scenes[0].camera
+    camera = svo_amd.PinholeCamera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"])
+
+    # device-resident inputs: 3 pyramids per pair, each pair in its own buffers
+    ps = svo_amd.PyramidSet(3 * P, cam["width"], cam["height"], L, ctx)
+    base = np.stack([im for s in scenes for im in (s.ref_img, s.kf_img, s.cur_img)])
+    for first in range(0, P, D):
+        cnt = min(D, P - first)
+        ps.upload(3 * first, base[:3 * cnt])
+    ctx.synchronize()
+    ctx.record(2)
+    ps.build()
+    ctx.record(3)
+    pyr_ms = ctx.elapsed_ms(2, 3)
+
+    batch = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx)
+    for i in range(P):
+        s = scenes[i % D]
+        batch.set_pair(i, (ps, 3 * i), (ps, 3 * i + 1), (ps, 3 * i + 2), s.ref_pose, s.kf_pose, s.cur_init_pose,
+                       s.n_ref, s.n_kf, s.px, s.bearing, s.point, s.has_point)
+
+    for _ in range(args.warmup):
+        batch.run()
+    ctx.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ctx.record(0)
+    for _ in range(args.steps):
+        batch.run()
+    ctx.record(1)
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    kernel_ms = ctx.elapsed_ms(0, 1) / args.steps
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    poses, err, status = batch.results()
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    value = world * P * args.steps / elapsed
+    b_pair = 3 * level_bytes(cam["width"], cam["height"], L) + nf * 64
+    achieved = b_pair * P / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if args.pmc_json and os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"config 2: ImageAlignment::align, {nf} feats ({nf // 2} ref + {nf - nf // 2} lastKF), "
+                               f"patch {patch}, {L}-level pyramid, {cam['width']}x{cam['height']}, {P} pairs/GPU",
+                   "pairs_per_gpu": P, "features": nf, "levels": L, "patch": patch, "distinct_scenes": D,
+                   "parallelism": f"pairs sharded over {world} GPU(s), no collective"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "kernel": "align_pairs_kernel", "kernel_ms": round(kernel_ms, 4),
+                     "algorithmic_bytes_per_pair": b_pair},
+        "pyramid_build": {"frames": 3 * P, "ms": round(pyr_ms, 4),
+                          "frames_per_s": round(3 * P / (pyr_ms * 1e-3), 1)},
+        "status_counts": {svo_amd.STATUS_NAMES[int(k)]: int(v) for k, v in zip(*np.unique(status, return_counts=True))},
+    }
+    if not args.no_cpu and world == 1:
+        out.update(cpu_baseline(args, scenes, poses, L, patch, nthreads))
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, scenes, gpu_poses, L, patch, nthreads):
+    """The oracle (faithful C++ restatement, -O3) timed on this host on a bounded sample of the same
+    workload; also the SE(3) error of the GPU poses vs the reference semantics on those pairs."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # noqa: E402  (CPU baseline / checker only)
+    pyrs = [[O.build_pyramid(im, L)[0] for im in (s.ref_img, s.kf_img, s.cur_img)] for s in scenes]
+    pairs = [O.make_pair(p[0], p[1], p[2], s.ref_pose, s.kf_pose, s.n_ref, s.n_kf, s.px, s.bearing, s.point, s.has_point)
+             for p, s in zip(pyrs, scenes)]
+    # single core: whole alignments until the budget is spent
+    done, t0, se3_err = 0, time.perf_counter(), 0.0
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        i = done % len(scenes)
+        pose, _, _, _ = O.image_align(scenes[i].camera, patch, 0, L - 1, pairs[i], scenes[i].cur_init_pose, 0)
+        if done < len(scenes):
+            a, b = np.array(pose), np.array(gpu_poses[i])
+            if a[3] < 0:
+                a[:4] = -a[:4]
+            if b[3] < 0:
+                b[:4] = -b[:4]
+            se3_err = max(se3_err, float(np.abs(a - b).max()))
+        done += 1
+    single = done / (time.perf_counter() - t0)
+    # all requested threads: one independent alignment per thread (the reference runs align on one thread)
+    n_mt = max(nthreads, 2) * max(4, int(single * args.cpu_seconds / 8))
+    idx = [i % len(scenes) for i in range(n_mt)]
+    t0 = time.perf_counter()
+    O.image_align_batch(scenes[0].camera, patch, 0, L - 1, [pairs[i] for i in idx],
+                        np.stack([scenes[i].cur_init_pose for i in idx]), 0, args.cpu_threads)
+    multi = n_mt / (time.perf_counter() - t0)
+    return {
+        "cpu_baseline": {"value": round(single, 3), "unit": "pairs/s", "cores": 1, "kind": "port",
+                         "sample": f"{done} whole ImageAlignment::align calls (config 2 shape, {len(scenes)} scenes) "
+                                   f"in {args.cpu_seconds:.0f} s on 1 host thread, oracle/svo_oracle.cpp -O3"},
+        "cpu_baseline_multicore": {"value": round(multi, 3), "unit": "pairs/s", "cores": args.cpu_threads,
+                                   "kind": "port", "sample": f"{n_mt} alignments, one per thread at a time"},
+        "se3_err_vs_ref": {"max_abs_param_diff": se3_err, "pairs": min(done, len(scenes)),
+                           "reference_semantics": "libstdc++ nth_element median (median_mode 0)"},
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,165 @@
+/*
+ * svo_c.h — C ABI of the MI355X-native direct-alignment hot path (libsvo_hip.so).
+ *
+ * This is the drop-in boundary for amin-abouee/semi-direct-visual-odometry's sparse image alignment,
+ * feature alignment and image pyramid.  The reference has no plugin registry or FFI: its boundary is
+ * the C++ class surface.  Each entry point below names the reference interface it
+ * replaces (paths relative to the reference root).  The C++ host mirror of that class surface
+ * (semi-direct-visual-odometry_amd/host/svo.hpp) and the Python mirror (svo_amd) sit on top of it.
+ *
+ * Conventions
+ *   - every function returns int: 0 = SVO_OK, < 0 = error (svo_last_error() has the message);
+ *     no C++ exception crosses the ABI;
+ *   - host buffers are caller-owned and only read/written during the call (or until the documented
+ *     synchronisation point for *_run);
+ *   - device memory is owned by the context; one context per (host thread, GPU); not reentrant;
+ *   - poses are world->camera SE(3) in Sophus params() order: qx, qy, qz, qw, tx, ty, tz
+ *     (Frame::m_absPose, include/frame.hpp:198);
+ *   - images are 8-bit grey, row-major, tightly packed (cv::Mat CV_8UC1, continuous).
+ */
+#ifndef SVO_C_H
+#define SVO_C_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVO_ABI_VERSION 1
+
+enum {
+    SVO_OK = 0,
+    SVO_ERR_ARG = -1,    /* bad argument (null pointer, size out of range, bad index) */
+    SVO_ERR_HIP = -2,    /* HIP runtime error */
+    SVO_ERR_NODEV = -3,  /* no usable gfx950 device */
+    SVO_ERR_STATE = -4   /* object used in the wrong state (e.g. results before run) */
+};
+
+/* Optimizer::Status values (include/optimizer.hpp:21-33) reported per alignment. */
+enum {
+    SVO_STATUS_SUCCESS = 0,
+    SVO_STATUS_MAX_COFF_DX = 1,
+    SVO_STATUS_NON_IN_DX = 2,
+    SVO_STATUS_SMALL_STEP_SIZE = 3,
+    SVO_STATUS_LAMBDA_VALUE = 4,
+    SVO_STATUS_NORM_INF_DIFF = 5,
+    SVO_STATUS_NON_SUFF_POINTS = 6,
+    SVO_STATUS_INCREASE_CHI_SQUARED_ERROR = 7,
+    SVO_STATUS_SMALL_CHI_SQUARED_ERROR = 8,
+    SVO_STATUS_FAILED = 9
+};
+
+typedef struct svo_ctx svo_ctx;
+typedef struct svo_pyramid_set svo_pyramid_set;
+typedef struct svo_align_batch svo_align_batch;
+
+/* PinholeCamera without distortion (src/pinhole_camera.cpp:50-101; KITTI d = 0, resource/kitti.yaml). */
+typedef struct {
+    double fx, fy, cx, cy;
+    int32_t width, height;
+} svo_camera;
+
+/* ImageAlignment(patchSize, minLevel, maxLevel, numParameters=6) (include/image_alignment.hpp:18).
+ * median_mode: 0 = exact order statistics for the Tukey scale (the only mode implemented; the
+ * reference's libstdc++ nth_element neighbour read is within the pose tolerance). */
+typedef struct {
+    int32_t patch_size;
+    int32_t min_level;
+    int32_t max_level;
+    int32_t median_mode;
+} svo_align_params;
+
+/* Per pair, per pyramid level record of the single LM step (mirrors Optimizer state after
+ * optimizeLM, src/optimizer.cpp:162-370).  H is the damped 6x6 (row-major), g the gradient. */
+typedef struct {
+    int32_t level, n_ref_vis, n_vis, status;
+    double median, mad, sigma, chi2, lambda, err;
+    double H[36], g[6], dx[6];
+} svo_level_trace;
+
+/* ---------------------------------------------------------------- context */
+int svo_device_count(int32_t* count);
+int svo_ctx_create(int32_t device, svo_ctx** out);
+int svo_ctx_destroy(svo_ctx* ctx);
+int svo_ctx_synchronize(svo_ctx* ctx);
+/* hipStream_t of the context (all work of the context is enqueued on it), for event timing. */
+void* svo_ctx_stream(svo_ctx* ctx);
+const char* svo_last_error(void);
+int svo_abi_version(void);
+/* hipEvent timing on the context stream: record event `slot` (0..15) now; elapsed ms between two
+ * recorded slots (waits for the later one). */
+int svo_ctx_event_record(svo_ctx* ctx, int32_t slot);
+int svo_ctx_event_elapsed(svo_ctx* ctx, int32_t slot_begin, int32_t slot_end, float* ms);
+
+/* ---------------------------------------------------------------- ImagePyramid
+ * Replaces ImagePyramid::createImagePyramid (src/image_pyramid.cpp:36-52), called from the Frame
+ * constructor (src/frame.cpp:26): per frame an intensity stack (level 0 = input, level l = pyrDown
+ * of level l-1) and a gradient stack (level 0 = Simd::AbsGradientSaturatedSum, level l = pyrDown of
+ * gradient l-1).  A set holds n_frames device-resident stacks of equal geometry, packed level after
+ * level; level sizes are ((w+1)/2, (h+1)/2) per step (cv::pyrDown default). */
+int svo_pyramid_set_create(svo_ctx* ctx, int32_t n_frames, int32_t width, int32_t height, int32_t levels,
+                           svo_pyramid_set** out);
+int svo_pyramid_set_destroy(svo_pyramid_set* set);
+/* Copy `count` base images (count*width*height bytes) into frames [first, first+count). Async. */
+int svo_pyramid_set_upload(svo_pyramid_set* set, int32_t first, int32_t count, const uint8_t* host_images);
+/* Same, from device memory (e.g. a decoder's output), stream-ordered. */
+int svo_pyramid_set_upload_device(svo_pyramid_set* set, int32_t first, int32_t count, const uint8_t* dev_images);
+/* Build both stacks for frames [first, first+count) on the device.  Async (context stream). */
+int svo_pyramid_set_build(svo_pyramid_set* set, int32_t first, int32_t count);
+/* ImagePyramid::getImageAtLevel / getGradientAtLevel (src/image_pyramid.cpp:54-124): copy one level
+ * to the host (synchronous).  gradient = 0 for the intensity stack, 1 for the gradient stack. */
+int svo_pyramid_set_download(const svo_pyramid_set* set, int32_t frame, int32_t level, int32_t gradient, uint8_t* out);
+/* ImagePyramid::getImageSizeAtLevel (src/image_pyramid.cpp:110-116). */
+int svo_pyramid_level_size(const svo_pyramid_set* set, int32_t level, int32_t* width, int32_t* height);
+
+/* ---------------------------------------------------------------- ImageAlignment
+ * Replaces ImageAlignment::align(refFrame, curFrame) (src/image_alignment.cpp:25-67, declared
+ * include/image_alignment.hpp:25; called src/system.cpp:313).  A batch holds n_pairs independent
+ * (ref, ref->lastKeyframe, cur) problems; each is the reference's whole coarse-to-fine call:
+ * for level = max..min: Jacobian of the ref patches, one Tukey-weighted Nielsen-damped LM step,
+ * pose <- pose * exp(-dx).  Features are the ref frame's, then the last keyframe's, in vector order
+ * (slots exist for features without a point, src/image_alignment.cpp:81-121). */
+int svo_align_batch_create(svo_ctx* ctx, const svo_camera* cam, const svo_align_params* params, int32_t n_pairs,
+                           int32_t max_features, svo_align_batch** out);
+int svo_align_batch_destroy(svo_align_batch* batch);
+/* Describe pair `pair`: each frame is (pyramid set, frame index); the sets must outlive the batch's runs.
+ *   px       (n_ref+n_kf) x 2   Feature::m_pixelPosition at level 0 (include/feature.hpp:31)
+ *   bearing  (n_ref+n_kf) x 3   Feature::m_bearingVec (include/feature.hpp:33-34)
+ *   point    (n_ref+n_kf) x 3   Point::m_position in world coordinates (include/point.hpp:28)
+ *   has_point(n_ref+n_kf)       Feature::m_point != nullptr
+ * Copies the host arrays to device memory (synchronous). */
+int svo_align_batch_set_pair(svo_align_batch* batch, int32_t pair, const svo_pyramid_set* ref_set, int32_t ref_frame,
+                             const svo_pyramid_set* kf_set, int32_t kf_frame, const svo_pyramid_set* cur_set,
+                             int32_t cur_frame, const double* ref_pose, const double* kf_pose,
+                             const double* cur_pose, int32_t n_ref, int32_t n_kf, const double* px,
+                             const double* bearing, const double* point, const uint8_t* has_point);
+/* Replace the initial cur poses of all pairs (n_pairs x 7).  Synchronous H2D. */
+int svo_align_batch_set_initial_poses(svo_align_batch* batch, const double* poses);
+/* Run every pair.  Asynchronous on the context stream; inputs stay untouched, so repeated runs are
+ * identical (the result pose is written to a separate device buffer). */
+int svo_align_batch_run(svo_align_batch* batch);
+/* Wait for the last run and copy results: poses n_pairs x 7 (the aligned cur->m_absPose), err
+ * n_pairs (the RMSE of the finest level, as align() returns), status n_pairs (Optimizer::Status of
+ * the finest level).  Any pointer may be NULL. */
+int svo_align_batch_results(svo_align_batch* batch, double* poses, double* err, int32_t* status);
+/* Per-level records of one pair (max_level+1 entries, indexed by level). */
+int svo_align_batch_traces(svo_align_batch* batch, int32_t pair, svo_level_trace* out);
+
+/* ---------------------------------------------------------------- FeatureAlignment
+ * Replaces FeatureAlignment::align(refFeature, curFrame, pixelPos) (src/feature_alignment.cpp:25-62,
+ * declared include/feature_alignment.hpp:25; called src/map.cpp:538,608) for n candidates at once:
+ * 2-D translation + intensity bias on the level-0 GRADIENT images of the ref and cur frames, one
+ * LM step, pixelPos <- flow.xy.  Candidate i's reference feature lives in frame ref_frames[i]
+ * (refFeature->m_frame; NULL = every candidate in ref_frame) at ref_px[i] (its m_pixelPosition).
+ * px_inout: n x 2 (initial pixel positions in, aligned out); err: the returned RMSE (NaN when the
+ * patch left the frame); status: Optimizer::Status.  Synchronous. */
+int svo_feature_align(svo_ctx* ctx, const svo_camera* cam, int32_t patch_size, const svo_pyramid_set* ref_set,
+                      const int32_t* ref_frames, int32_t ref_frame, const svo_pyramid_set* cur_set, int32_t cur_frame,
+                      int32_t n, const double* ref_px, double* px_inout, double* err, int32_t* status);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SVO_C_H */

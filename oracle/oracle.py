@@ -1,0 +1,203 @@
+"""ctypes wrapper for the CPU oracle (oracle/svo_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker / CPU baseline.  The product path never imports this module.
+
+Parity status: partially pinned.  The reference cannot be compiled here (OpenCV, Eigen, Sophus, g2o
+and the prebuilt Simd/CHOLMOD libraries are absent), so the restatement is pinned by
+(i) the reference's own known-answer test for the projection (tests/test_camera.cpp:94-95) and its
+pyramid structure tests (tests/test_image_pyramid.cpp:27-60), and (ii) independent restatements of the
+third-party arithmetic (numpy pyrDown / abs-gradient, scipy rotations for SE3 exp, numpy solve for
+LDLT, real libstdc++ nth_element) — see tests/test_oracle_kats.py.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libsvo_oracle.so")
+_lib = None
+
+
+class OcCamera(ctypes.Structure):
+    _fields_ = [("fx", ctypes.c_double), ("fy", ctypes.c_double), ("cx", ctypes.c_double), ("cy", ctypes.c_double),
+                ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
+
+
+class OcPair(ctypes.Structure):
+    _fields_ = [("ref_pyr", ctypes.c_void_p), ("kf_pyr", ctypes.c_void_p), ("cur_pyr", ctypes.c_void_p),
+                ("ref_pose", ctypes.c_double * 7), ("kf_pose", ctypes.c_double * 7),
+                ("n_ref", ctypes.c_int32), ("n_kf", ctypes.c_int32),
+                ("px", ctypes.c_void_p), ("bearing", ctypes.c_void_p), ("point", ctypes.c_void_p),
+                ("has_point", ctypes.c_void_p)]
+
+
+class LevelTrace(ctypes.Structure):
+    _fields_ = [("level", ctypes.c_int32), ("n_ref_vis", ctypes.c_int32), ("n_vis", ctypes.c_int32),
+                ("status", ctypes.c_int32), ("median", ctypes.c_double), ("mad", ctypes.c_double),
+                ("sigma", ctypes.c_double), ("chi2", ctypes.c_double), ("lambda_", ctypes.c_double),
+                ("err", ctypes.c_double), ("H", ctypes.c_double * 36), ("g", ctypes.c_double * 6),
+                ("dx", ctypes.c_double * 6)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_pyramid_bytes.restype = ctypes.c_int64
+        L.oracle_image_align.restype = ctypes.c_double
+        L.oracle_median.restype = ctypes.c_double
+        L.oracle_median.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32]
+        L.oracle_bilinear_d.restype = ctypes.c_double
+        L.oracle_bilinear_d.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double]
+        L.oracle_bilinear_f.restype = ctypes.c_float
+        L.oracle_bilinear_f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double]
+        assert L.oracle_level_trace_size() == ctypes.sizeof(LevelTrace)
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def camera(cam):
+    return OcCamera(cam["fx"], cam["fy"], cam["cx"], cam["cy"], cam["width"], cam["height"])
+
+
+def pyramid_bytes(w, h, levels):
+    return lib().oracle_pyramid_bytes(w, h, levels)
+
+
+def build_pyramid(img, levels):
+    """ImagePyramid::createImagePyramid -> (packed image stack, packed gradient stack)."""
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    n = pyramid_bytes(w, h, levels)
+    out_i = np.zeros(n, np.uint8)
+    out_g = np.zeros(n, np.uint8)
+    lib().oracle_build_pyramid(_p(img), w, h, levels, _p(out_i), _p(out_g))
+    return out_i, out_g
+
+
+def level_shapes(w, h, levels):
+    shapes, off = [], 0
+    for _ in range(levels):
+        shapes.append((h, w, off))
+        off += w * h
+        w, h = (w + 1) // 2, (h + 1) // 2
+    return shapes
+
+
+def unpack_levels(packed, w, h, levels):
+    return [packed[o:o + hh * ww].reshape(hh, ww) for hh, ww, o in level_shapes(w, h, levels)]
+
+
+def project2d(cam, p3):
+    out = np.zeros(2)
+    p3 = np.ascontiguousarray(p3, dtype=np.float64)
+    lib().oracle_project2d(ctypes.byref(camera(cam)), _p(p3), _p(out))
+    return out
+
+
+def se3_exp(tangent):
+    t = np.ascontiguousarray(tangent, dtype=np.float64)
+    out = np.zeros(7)
+    lib().oracle_se3_exp(_p(t), _p(out))
+    return out
+
+
+def se3_compose(a, b):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    out = np.zeros(7)
+    lib().oracle_se3_compose(_p(a), _p(b), _p(out))
+    return out
+
+
+def ldlt_solve(H, b):
+    H = np.ascontiguousarray(H, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    x = np.zeros(len(b))
+    lib().oracle_ldlt_solve(len(b), _p(H), _p(b), _p(x))
+    return x
+
+
+def median(v, n_valid, mode=0):
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    return lib().oracle_median(_p(v), len(v), n_valid, mode)
+
+
+def bilinear_d(img, x, y):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    return lib().oracle_bilinear_d(_p(img), img.shape[1], img.shape[0], x, y)
+
+
+def bilinear_f(img, x, y):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    return lib().oracle_bilinear_f(_p(img), img.shape[1], img.shape[0], x, y)
+
+
+class _PairKeep:
+    """Keeps numpy buffers alive while an OcPair points into them."""
+
+    def __init__(self, pair, keep):
+        self.pair = pair
+        self.keep = keep
+
+
+def make_pair(ref_pyr, kf_pyr, cur_pyr, ref_pose, kf_pose, n_ref, n_kf, px, bearing, point, has_point):
+    keep = [np.ascontiguousarray(a) for a in (ref_pyr, kf_pyr, cur_pyr)]
+    feats = [np.ascontiguousarray(px, np.float64), np.ascontiguousarray(bearing, np.float64),
+             np.ascontiguousarray(point, np.float64), np.ascontiguousarray(has_point, np.uint8)]
+    P = OcPair()
+    P.ref_pyr, P.kf_pyr, P.cur_pyr = (_p(a).value for a in keep)
+    P.ref_pose[:] = list(ref_pose)
+    P.kf_pose[:] = list(kf_pose)
+    P.n_ref, P.n_kf = int(n_ref), int(n_kf)
+    P.px, P.bearing, P.point, P.has_point = (_p(a).value for a in feats)
+    return _PairKeep(P, keep + feats)
+
+
+def image_align(cam, patch, min_level, max_level, pair, cur_pose, median_mode=0, trace=False):
+    """ImageAlignment::align.  Returns (pose[7], err, status, traces or None)."""
+    pose = np.ascontiguousarray(cur_pose, dtype=np.float64).copy()
+    st = ctypes.c_int32()
+    traces = (LevelTrace * (max_level + 1))() if trace else None
+    err = lib().oracle_image_align(ctypes.byref(camera(cam)), patch, min_level, max_level, median_mode,
+                                   ctypes.byref(pair.pair), _p(pose), ctypes.byref(st),
+                                   ctypes.cast(traces, ctypes.c_void_p) if trace else None)
+    return pose, err, st.value, traces
+
+
+def image_align_batch(cam, patch, min_level, max_level, pairs, cur_poses, median_mode=0, nthreads=1):
+    n = len(pairs)
+    arr = (OcPair * n)(*[p.pair for p in pairs])
+    poses = np.ascontiguousarray(cur_poses, dtype=np.float64).copy()
+    err = np.zeros(n)
+    st = np.zeros(n, np.int32)
+    lib().oracle_image_align_batch(ctypes.byref(camera(cam)), patch, min_level, max_level, median_mode, n, arr,
+                                   _p(poses), _p(err), _p(st), nthreads)
+    return poses, err, st
+
+
+def feature_align(cam, patch, ref_grad, cur_grad, ref_px, px_init):
+    """FeatureAlignment::align for n candidates.  Returns (px[n,2], err[n], status[n])."""
+    ref_grad = np.ascontiguousarray(ref_grad, np.uint8)
+    cur_grad = np.ascontiguousarray(cur_grad, np.uint8)
+    ref_px = np.ascontiguousarray(ref_px, np.float64)
+    px = np.ascontiguousarray(px_init, np.float64).copy()
+    n = len(px)
+    err = np.zeros(n)
+    st = np.zeros(n, np.int32)
+    lib().oracle_feature_align(ctypes.byref(camera(cam)), patch, _p(ref_grad), _p(cur_grad), n, _p(ref_px), _p(px),
+                               _p(err), _p(st))
+    return px, err, st

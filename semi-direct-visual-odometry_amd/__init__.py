@@ -1,0 +1,11 @@
+"""svo_amd — MI355X-native direct-alignment hot path of amin-abouee/semi-direct-visual-odometry.
+
+Product path: HIP kernels in libsvo_hip.so behind the C ABI of include/svo_c.h.  This package mirrors the
+reference's ImagePyramid / ImageAlignment / FeatureAlignment class surface over that ABI (core.py).
+"""
+from .core import (AlignBatch, Context, Feature, FeatureAlignment, Frame, ImageAlignment, ImagePyramid,
+                   PinholeCamera, Point, PyramidSet, default_context, device_count)
+from ._capi import STATUS_NAMES, SvoError
+
+__all__ = ["AlignBatch", "Context", "Feature", "FeatureAlignment", "Frame", "ImageAlignment", "ImagePyramid",
+           "PinholeCamera", "Point", "PyramidSet", "default_context", "device_count", "STATUS_NAMES", "SvoError"]

@@ -1,0 +1,371 @@
+"""Python mirror of the reference's class surface for the alignment hot path, over the C ABI.
+
+Names, argument meaning and error behaviour follow the reference:
+  PinholeCamera      include/pinhole_camera.hpp:16 (undistorted path, src/pinhole_camera.cpp:50-101)
+  ImagePyramid       include/image_pyramid.hpp:23-149          (device resident; getters download)
+  Frame / Feature / Point   include/frame.hpp:70-208, include/feature.hpp:14, include/point.hpp:14
+  ImageAlignment     include/image_alignment.hpp:15-73         (align(ref, cur) -> error, cur pose in place)
+  FeatureAlignment   include/feature_alignment.hpp:15-43       (align(feature, cur, px) -> error, px in place)
+plus the batched forms the GPU is built for (AlignBatch, FeatureAlignment.align_batch).
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, lib, ptr
+
+_default_ctx = {}
+
+
+class Context:
+    """One HIP stream on one GPU (svo_ctx)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(lib().svo_ctx_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = int(device)
+
+    @property
+    def stream(self):
+        return lib().svo_ctx_stream(self.handle)
+
+    def synchronize(self):
+        check(lib().svo_ctx_synchronize(self.handle))
+
+    def record(self, slot):
+        """hipEventRecord(slot) on this context's stream."""
+        check(lib().svo_ctx_event_record(self.handle, int(slot)))
+
+    def elapsed_ms(self, a, b):
+        ms = ctypes.c_float()
+        check(lib().svo_ctx_event_elapsed(self.handle, int(a), int(b), ctypes.byref(ms)))
+        return ms.value
+
+    def close(self):
+        if self.handle:
+            lib().svo_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def default_context(device=0):
+    if device not in _default_ctx:
+        _default_ctx[device] = Context(device)
+    return _default_ctx[device]
+
+
+def device_count():
+    n = ctypes.c_int32()
+    check(lib().svo_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class PinholeCamera:
+    def __init__(self, width, height, fx, fy, cx, cy):
+        self.width, self.height = int(width), int(height)
+        self.fx, self.fy, self.cx, self.cy = float(fx), float(fy), float(cx), float(cy)
+
+    @classmethod
+    def kitti(cls):  # resource/kitti.yaml:7-8, config/config.json:10-11
+        return cls(1241, 376, 721.5377, 721.5377, 609.5593, 172.8540)
+
+    def as_c(self):
+        return _capi.SvoCamera(self.fx, self.fy, self.cx, self.cy, self.width, self.height)
+
+    def as_dict(self):
+        return dict(fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy, width=self.width, height=self.height)
+
+    def project2d(self, p):  # src/pinhole_camera.cpp:53-57
+        return np.array([self.fx * (p[0] / p[2]) + self.cx, self.fy * (p[1] / p[2]) + self.cy])
+
+    def inverse_project2d(self, px):  # src/pinhole_camera.cpp:84-100
+        v = np.array([(px[0] - self.cx) / self.fx, (px[1] - self.cy) / self.fy, 1.0])
+        return v * (1.0 / math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]))
+
+    def is_in_frame(self, p, boundary=0.0):  # src/pinhole_camera.cpp:163-168
+        return p[0] >= boundary and p[1] >= boundary and p[0] < self.width - boundary and p[1] < self.height - boundary
+
+
+class PyramidSet:
+    """n_frames device-resident (image, gradient) stacks of equal geometry (svo_pyramid_set)."""
+
+    def __init__(self, n_frames, width, height, levels, ctx=None):
+        self.ctx = ctx or default_context()
+        self.n_frames, self.width, self.height, self.levels = int(n_frames), int(width), int(height), int(levels)
+        h = ctypes.c_void_p()
+        check(lib().svo_pyramid_set_create(self.ctx.handle, self.n_frames, self.width, self.height, self.levels,
+                                           ctypes.byref(h)))
+        self.handle = h
+
+    def upload(self, first, images):
+        imgs = np.ascontiguousarray(images, dtype=np.uint8)
+        count = imgs.shape[0] if imgs.ndim == 3 else 1
+        if imgs.shape[-2:] != (self.height, self.width):
+            raise ValueError(f"image shape {imgs.shape[-2:]} != ({self.height}, {self.width})")
+        check(lib().svo_pyramid_set_upload(self.handle, int(first), count, ptr(imgs)))
+        self.ctx.synchronize()  # the host buffer may die after return
+
+    def build(self, first=0, count=None):
+        count = self.n_frames - first if count is None else count
+        check(lib().svo_pyramid_set_build(self.handle, int(first), int(count)))
+
+    def level_size(self, level):
+        w, h = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().svo_pyramid_level_size(self.handle, int(level), ctypes.byref(w), ctypes.byref(h)))
+        return w.value, h.value
+
+    def download(self, frame, level, gradient=False):
+        w, h = self.level_size(level)
+        out = np.empty((h, w), np.uint8)
+        check(lib().svo_pyramid_set_download(self.handle, int(frame), int(level), 1 if gradient else 0, ptr(out)))
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().svo_pyramid_set_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ImagePyramid:
+    """ImagePyramid(baseImage, maxPyramidLevel) — device resident (src/image_pyramid.cpp:14-52)."""
+
+    def __init__(self, base_image=None, levels=4, ctx=None):
+        self.ctx = ctx or default_context()
+        self.levels = int(levels)
+        self.set = None
+        if base_image is not None:
+            self.create_image_pyramid(base_image, levels)
+
+    def create_image_pyramid(self, base_image, levels):
+        img = np.ascontiguousarray(base_image, dtype=np.uint8)
+        if img.ndim != 2:
+            raise ValueError("ImagePyramid expects one 8-bit grey image")
+        self.levels = int(levels)
+        self.set = PyramidSet(1, img.shape[1], img.shape[0], self.levels, self.ctx)
+        self.set.upload(0, img[None])
+        self.set.build(0, 1)
+
+    def get_size_image_pyramid(self):
+        return 0 if self.set is None else self.levels
+
+    def get_image_at_level(self, level):
+        return self.set.download(0, level, False)
+
+    def get_gradient_at_level(self, level):
+        return self.set.download(0, level, True)
+
+    def get_base_image(self):
+        return self.get_image_at_level(0)
+
+    def get_base_gradient_image(self):
+        return self.get_gradient_at_level(0)
+
+    def get_image_size_at_level(self, level):
+        if self.set is None or level >= self.levels:
+            return (0, 0)
+        return self.set.level_size(level)
+
+    def get_base_image_size(self):
+        return self.get_image_size_at_level(0)
+
+    def clear(self):
+        if self.set is not None:
+            self.set.close()
+        self.set = None
+
+
+class Point:
+    def __init__(self, position):
+        self.position = np.asarray(position, dtype=np.float64)
+
+
+class Feature:
+    """Feature(frame, pixelPosition, level) — bearing from the frame's camera (src/feature.cpp:14)."""
+
+    def __init__(self, frame, pixel_position, level=0, point=None, bearing=None):
+        self.frame = frame
+        self.pixel_position = np.asarray(pixel_position, dtype=np.float64)
+        self.level = level
+        self.bearing_vec = (np.asarray(bearing, np.float64) if bearing is not None
+                            else frame.camera.inverse_project2d(self.pixel_position))
+        self.point = point
+
+    def set_point(self, point):
+        self.point = point
+
+
+class Frame:
+    """Frame(camera, img, maxImagePyramid, timestamp, lastKeyframe) (src/frame.cpp:6-27)."""
+
+    def __init__(self, camera, image, max_image_pyramid, timestamp=0, last_keyframe=None, ctx=None):
+        img = np.asarray(image)
+        if img.dtype != np.uint8 or img.ndim != 2 or img.shape != (camera.height, camera.width):
+            raise RuntimeError("Image Corrupted")  # src/frame.cpp:20-24
+        self.camera = camera
+        self.abs_pose = np.array([0, 0, 0, 1, 0, 0, 0], dtype=np.float64)  # identity (src/frame.cpp:13)
+        self.image_pyramid = ImagePyramid(img, max_image_pyramid, ctx)
+        self.features = []
+        self.last_keyframe = last_keyframe
+        self.timestamp = timestamp
+
+    def add_feature(self, feature):
+        self.features.append(feature)
+
+    def number_observation(self):
+        return len(self.features)
+
+
+def _feature_arrays(frames):
+    feats = [f for fr in frames for f in fr.features]
+    n = len(feats)
+    px = np.zeros((max(n, 1), 2))
+    br = np.zeros((max(n, 1), 3))
+    pt = np.zeros((max(n, 1), 3))
+    hp = np.zeros(max(n, 1), np.uint8)
+    for i, f in enumerate(feats):
+        px[i] = f.pixel_position
+        br[i] = f.bearing_vec
+        if f.point is not None:
+            pt[i] = f.point.position
+            hp[i] = 1
+    return px, br, pt, hp
+
+
+class AlignBatch:
+    """n_pairs independent ImageAlignment::align problems on one GPU (svo_align_batch)."""
+
+    def __init__(self, camera, patch_size, min_level, max_level, n_pairs, max_features, ctx=None):
+        self.ctx = ctx or default_context()
+        self.camera = camera
+        self.n_pairs = int(n_pairs)
+        self.max_level = int(max_level)
+        self._c_cam = camera.as_c()
+        self._c_prm = _capi.SvoAlignParams(int(patch_size), int(min_level), int(max_level), 0)
+        h = ctypes.c_void_p()
+        check(lib().svo_align_batch_create(self.ctx.handle, ctypes.byref(self._c_cam), ctypes.byref(self._c_prm),
+                                           self.n_pairs, int(max_features), ctypes.byref(h)))
+        self.handle = h
+        self._keep = {}
+
+    def set_pair(self, pair, ref, kf, cur, ref_pose, kf_pose, cur_pose, n_ref, n_kf, px, bearing, point, has_point):
+        """ref/kf/cur: (PyramidSet, frame index)."""
+        arr = lambda a, dt: np.ascontiguousarray(a, dtype=dt)
+        px, bearing, point, has_point = arr(px, np.float64), arr(bearing, np.float64), arr(point, np.float64), \
+            arr(has_point, np.uint8)
+        poses = [arr(p, np.float64) for p in (ref_pose, kf_pose, cur_pose)]
+        check(lib().svo_align_batch_set_pair(self.handle, int(pair), ref[0].handle, int(ref[1]), kf[0].handle,
+                                             int(kf[1]), cur[0].handle, int(cur[1]), *[ptr(p) for p in poses],
+                                             int(n_ref), int(n_kf), ptr(px), ptr(bearing), ptr(point), ptr(has_point)))
+        self._keep[pair] = (ref[0], kf[0], cur[0])
+
+    def set_initial_poses(self, poses):
+        poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(self.n_pairs, 7)
+        check(lib().svo_align_batch_set_initial_poses(self.handle, ptr(poses)))
+
+    def run(self):
+        check(lib().svo_align_batch_run(self.handle))
+
+    def results(self):
+        poses = np.zeros((self.n_pairs, 7))
+        err = np.zeros(self.n_pairs)
+        st = np.zeros(self.n_pairs, np.int32)
+        check(lib().svo_align_batch_results(self.handle, ptr(poses), ptr(err), ptr(st)))
+        return poses, err, st
+
+    def traces(self, pair):
+        out = (_capi.SvoLevelTrace * (self.max_level + 1))()
+        check(lib().svo_align_batch_traces(self.handle, int(pair), ctypes.cast(out, ctypes.c_void_p)))
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().svo_align_batch_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ImageAlignment:
+    """ImageAlignment(patchSize, minLevel, maxLevel, numParameters) (src/image_alignment.cpp:15-67)."""
+
+    def __init__(self, patch_size, min_level, max_level, num_parameters=6, ctx=None):
+        if num_parameters != 6:
+            raise ValueError("ImageAlignment estimates SE(3): numParameters must be 6")
+        self.patch_size, self.min_level, self.max_level = int(patch_size), int(min_level), int(max_level)
+        self.ctx = ctx or default_context()
+        self.last_status = None
+        self.last_traces = None
+
+    def align(self, ref_frame, cur_frame):
+        """Aligns cur_frame.abs_pose in place; returns the finest level's RMSE (0 if ref has no features)."""
+        if ref_frame.number_observation() == 0:
+            return 0.0
+        kf = ref_frame.last_keyframe
+        if kf is None:
+            raise ValueError("ref_frame.last_keyframe is required (src/image_alignment.cpp:30-31)")
+        px, br, pt, hp = _feature_arrays([ref_frame, kf])
+        nf = ref_frame.number_observation() + kf.number_observation()
+        b = AlignBatch(ref_frame.camera, self.patch_size, self.min_level, self.max_level, 1, max(nf, 1), self.ctx)
+        try:
+            s = lambda fr: (fr.image_pyramid.set, 0)
+            b.set_pair(0, s(ref_frame), s(kf), s(cur_frame), ref_frame.abs_pose, kf.abs_pose, cur_frame.abs_pose,
+                       ref_frame.number_observation(), kf.number_observation(), px, br, pt, hp)
+            b.run()
+            poses, err, st = b.results()
+            self.last_traces = b.traces(0)
+        finally:
+            b.close()
+        cur_frame.abs_pose[:] = poses[0]
+        self.last_status = int(st[0])
+        return float(err[0])
+
+
+class FeatureAlignment:
+    """FeatureAlignment(patchSize, level, numParameters) (src/feature_alignment.cpp:15-62)."""
+
+    def __init__(self, patch_size, level=0, num_parameters=3, ctx=None):
+        if num_parameters != 3:
+            raise ValueError("FeatureAlignment estimates (u, v, bias): numParameters must be 3")
+        self.patch_size, self.level = int(patch_size), int(level)
+        self.ctx = ctx or default_context()
+        self.last_status = None
+
+    def align(self, ref_feature, cur_frame, pixel_pos):
+        """pixel_pos (numpy float64[2]) is updated in place; returns the RMSE (NaN if out of frame)."""
+        px = np.ascontiguousarray(pixel_pos, dtype=np.float64).reshape(1, 2).copy()
+        err, st = self.align_batch(ref_feature.frame.image_pyramid.set, [0], cur_frame.image_pyramid.set, 0,
+                                   ref_feature.pixel_position.reshape(1, 2), px, cur_frame.camera)
+        pixel_pos[0], pixel_pos[1] = px[0, 0], px[0, 1]
+        self.last_status = int(st[0])
+        return float(err[0])
+
+    def align_batch(self, ref_set, ref_frames, cur_set, cur_frame, ref_px, px_inout, camera):
+        ref_px = np.ascontiguousarray(ref_px, dtype=np.float64)
+        n = ref_px.shape[0]
+        if px_inout.dtype != np.float64 or not px_inout.flags.c_contiguous or px_inout.shape != (n, 2):
+            raise ValueError("px_inout must be a C-contiguous float64 (n, 2) array")
+        rf = np.ascontiguousarray(np.broadcast_to(np.asarray(ref_frames, np.int32), (n,)))
+        err = np.zeros(n)
+        st = np.zeros(n, np.int32)
+        cam = camera.as_c()
+        check(lib().svo_feature_align(self.ctx.handle, ctypes.byref(cam), self.patch_size, ref_set.handle, ptr(rf), 0,
+                                      cur_set.handle, int(cur_frame), n, ptr(ref_px), ptr(px_inout), ptr(err), ptr(st)))
+        return err, st

@@ -1,0 +1,458 @@
+// capi.hip — the C ABI (include/svo_c.h): contexts, device-resident pyramid sets, alignment batches.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "svo_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define SVO_HIP(call)                                                                                 \
+    do {                                                                                              \
+        hipError_t e_ = (call);                                                                       \
+        if (e_ != hipSuccess) return fail(SVO_ERR_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                                        \
+    } while (0)
+
+svo::LevelGeom make_geom(int32_t w, int32_t h, int32_t levels) {
+    svo::LevelGeom g{};
+    int64_t off = 0;
+    for (int l = 0; l < levels; ++l) {
+        g.w[l] = w; g.h[l] = h; g.off[l] = off;
+        off += (int64_t)w * h;
+        w = (w + 1) / 2;
+        h = (h + 1) / 2;
+    }
+    g.frame_bytes = off;
+    g.levels = levels;
+    return g;
+}
+
+}  // namespace
+
+struct svo_ctx {
+    int32_t device;
+    hipStream_t stream;
+    hipEvent_t events[16];
+};
+
+struct svo_pyramid_set {
+    svo_ctx* ctx;
+    int32_t n_frames, width, height, levels;
+    svo::LevelGeom geom;
+    int64_t grad_off, stride;
+    uint8_t* d_base;
+};
+
+struct svo_align_batch {
+    svo_ctx* ctx;
+    svo_camera cam;
+    svo_align_params params;
+    int32_t n_pairs, max_f, half, area;
+    svo::LevelGeom geom;
+    std::vector<svo::PairDesc> h_pairs;
+    std::vector<uint8_t> pair_set;
+    svo::PairDesc* d_pairs;
+    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_cuv, *d_res, *d_pose_out, *d_err;
+    uint8_t *d_has_point, *d_fvis;
+    int32_t* d_status;
+    svo_level_trace* d_traces;
+    bool ran;
+};
+
+extern "C" {
+
+const char* svo_last_error(void) { return g_err.c_str(); }
+int svo_abi_version(void) { return SVO_ABI_VERSION; }
+
+int svo_device_count(int32_t* count) {
+    if (!count) return fail(SVO_ERR_ARG, "count is null");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return SVO_OK;
+}
+
+int svo_ctx_create(int32_t device, svo_ctx** out) {
+    if (!out) return fail(SVO_ERR_ARG, "out is null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(SVO_ERR_NODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(SVO_ERR_ARG, "device %d out of range [0,%d)", device, n);
+    hipDeviceProp_t prop;
+    SVO_HIP(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SVO_ERR_NODEV, "device %d is %s; this build targets gfx950 (MI355X)", device, prop.gcnArchName);
+    SVO_HIP(hipSetDevice(device));
+    svo_ctx* c = new (std::nothrow) svo_ctx{};
+    if (!c) return fail(SVO_ERR_ARG, "out of host memory");
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 16 && e == hipSuccess; ++i) e = hipEventCreate(&c->events[i]);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(SVO_ERR_HIP, "hipStreamCreate/hipEventCreate: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return SVO_OK;
+}
+
+int svo_ctx_destroy(svo_ctx* c) {
+    if (!c) return SVO_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (hipEvent_t ev : c->events)
+        if (ev) (void)hipEventDestroy(ev);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SVO_OK;
+}
+
+int svo_ctx_synchronize(svo_ctx* c) {
+    if (!c) return fail(SVO_ERR_ARG, "ctx is null");
+    SVO_HIP(hipSetDevice(c->device));
+    SVO_HIP(hipStreamSynchronize(c->stream));
+    return SVO_OK;
+}
+
+void* svo_ctx_stream(svo_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int svo_ctx_event_record(svo_ctx* c, int32_t slot) {
+    if (!c || slot < 0 || slot >= 16) return fail(SVO_ERR_ARG, "bad context or event slot");
+    SVO_HIP(hipSetDevice(c->device));
+    SVO_HIP(hipEventRecord(c->events[slot], c->stream));
+    return SVO_OK;
+}
+
+int svo_ctx_event_elapsed(svo_ctx* c, int32_t a, int32_t b, float* ms) {
+    if (!c || !ms || a < 0 || a >= 16 || b < 0 || b >= 16) return fail(SVO_ERR_ARG, "bad context or event slot");
+    SVO_HIP(hipSetDevice(c->device));
+    SVO_HIP(hipEventSynchronize(c->events[b]));
+    SVO_HIP(hipEventElapsedTime(ms, c->events[a], c->events[b]));
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ pyramid sets
+int svo_pyramid_set_create(svo_ctx* c, int32_t n_frames, int32_t width, int32_t height, int32_t levels,
+                           svo_pyramid_set** out) {
+    if (!c || !out) return fail(SVO_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (n_frames <= 0 || width < 3 || height < 3 || levels < 1 || levels > svo::kMaxLevels)
+        return fail(SVO_ERR_ARG, "bad pyramid geometry n=%d %dx%d levels=%d", n_frames, width, height, levels);
+    SVO_HIP(hipSetDevice(c->device));
+    svo_pyramid_set* p = new (std::nothrow) svo_pyramid_set{};
+    if (!p) return fail(SVO_ERR_ARG, "out of host memory");
+    p->ctx = c;
+    p->n_frames = n_frames; p->width = width; p->height = height; p->levels = levels;
+    p->geom = make_geom(width, height, levels);
+    p->grad_off = (p->geom.frame_bytes + 255) / 256 * 256;
+    p->stride = (p->grad_off + p->geom.frame_bytes + 255) / 256 * 256;
+    hipError_t e = hipMalloc(&p->d_base, (size_t)p->stride * n_frames);
+    if (e != hipSuccess) {
+        delete p;
+        return fail(SVO_ERR_HIP, "hipMalloc(pyramids %lld B): %s", (long long)p->stride * n_frames, hipGetErrorString(e));
+    }
+    *out = p;
+    return SVO_OK;
+}
+
+int svo_pyramid_set_destroy(svo_pyramid_set* p) {
+    if (!p) return SVO_OK;
+    (void)hipSetDevice(p->ctx->device);
+    (void)hipStreamSynchronize(p->ctx->stream);
+    (void)hipFree(p->d_base);
+    delete p;
+    return SVO_OK;
+}
+
+static int upload_impl(svo_pyramid_set* p, int32_t first, int32_t count, const uint8_t* src, hipMemcpyKind kind) {
+    if (!p || !src) return fail(SVO_ERR_ARG, "null argument");
+    if (first < 0 || count < 0 || first + count > p->n_frames) return fail(SVO_ERR_ARG, "frames out of range");
+    SVO_HIP(hipSetDevice(p->ctx->device));
+    const size_t img = (size_t)p->width * p->height;
+    SVO_HIP(hipMemcpy2DAsync(p->d_base + (size_t)first * p->stride, (size_t)p->stride, src, img, img, count, kind,
+                             p->ctx->stream));
+    return SVO_OK;
+}
+
+int svo_pyramid_set_upload(svo_pyramid_set* p, int32_t first, int32_t count, const uint8_t* host_images) {
+    return upload_impl(p, first, count, host_images, hipMemcpyHostToDevice);
+}
+
+int svo_pyramid_set_upload_device(svo_pyramid_set* p, int32_t first, int32_t count, const uint8_t* dev_images) {
+    return upload_impl(p, first, count, dev_images, hipMemcpyDeviceToDevice);
+}
+
+int svo_pyramid_set_build(svo_pyramid_set* p, int32_t first, int32_t count) {
+    if (!p) return fail(SVO_ERR_ARG, "null argument");
+    if (first < 0 || count < 0 || first + count > p->n_frames) return fail(SVO_ERR_ARG, "frames out of range");
+    if (count == 0) return SVO_OK;
+    SVO_HIP(hipSetDevice(p->ctx->device));
+    svo::launch_pyramid(p->d_base, p->geom, first, count, p->ctx->stream);
+    SVO_HIP(hipGetLastError());
+    return SVO_OK;
+}
+
+int svo_pyramid_set_download(const svo_pyramid_set* p, int32_t frame, int32_t level, int32_t gradient, uint8_t* out) {
+    if (!p || !out) return fail(SVO_ERR_ARG, "null argument");
+    if (frame < 0 || frame >= p->n_frames || level < 0 || level >= p->levels) return fail(SVO_ERR_ARG, "index out of range");
+    SVO_HIP(hipSetDevice(p->ctx->device));
+    const uint8_t* src = p->d_base + (size_t)frame * p->stride + (gradient ? p->grad_off : 0) + p->geom.off[level];
+    SVO_HIP(hipMemcpyAsync(out, src, (size_t)p->geom.w[level] * p->geom.h[level], hipMemcpyDeviceToHost, p->ctx->stream));
+    SVO_HIP(hipStreamSynchronize(p->ctx->stream));
+    return SVO_OK;
+}
+
+int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, int32_t* h) {
+    if (!p || !w || !h) return fail(SVO_ERR_ARG, "null argument");
+    if (level < 0 || level >= p->levels) { *w = 0; *h = 0; return SVO_OK; }
+    *w = p->geom.w[level];
+    *h = p->geom.h[level];
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ image alignment batches
+static void free_batch(svo_align_batch* b) {
+    void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_jimg,
+                    b->d_cuv, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+}
+
+int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_params* prm, int32_t n_pairs,
+                           int32_t max_features, svo_align_batch** out) {
+    if (!c || !cam || !prm || !out) return fail(SVO_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (n_pairs <= 0 || max_features <= 0) return fail(SVO_ERR_ARG, "n_pairs and max_features must be > 0");
+    if (prm->patch_size < 1 || prm->patch_size > 31) return fail(SVO_ERR_ARG, "patch_size %d unsupported", prm->patch_size);
+    if (prm->min_level < 0 || prm->max_level < prm->min_level || prm->max_level >= svo::kMaxLevels)
+        return fail(SVO_ERR_ARG, "bad level range [%d,%d]", prm->min_level, prm->max_level);
+    if (prm->median_mode != 0) return fail(SVO_ERR_ARG, "median_mode %d not implemented (0 = exact)", prm->median_mode);
+    const int half = prm->patch_size / 2, area = (2 * half + 1) * (2 * half + 1);
+    if ((int64_t)max_features * area >= (1ll << 31)) return fail(SVO_ERR_ARG, "max_features too large");
+    SVO_HIP(hipSetDevice(c->device));
+    svo_align_batch* b = new (std::nothrow) svo_align_batch{};
+    if (!b) return fail(SVO_ERR_ARG, "out of host memory");
+    b->ctx = c; b->cam = *cam; b->params = *prm; b->n_pairs = n_pairs; b->max_f = max_features;
+    b->half = half; b->area = area;
+    b->geom = make_geom(cam->width, cam->height, prm->max_level + 1);
+    b->h_pairs.assign(n_pairs, svo::PairDesc{});
+    b->pair_set.assign(n_pairs, 0);
+    const size_t F = (size_t)n_pairs * max_features;
+    hipError_t e = hipSuccess;
+#define ALLOC(ptr, bytes) if (e == hipSuccess) e = hipMalloc(&ptr, bytes)
+    ALLOC(b->d_pairs, sizeof(svo::PairDesc) * n_pairs);
+    ALLOC(b->d_px, F * 2 * sizeof(double));
+    ALLOC(b->d_bearing, F * 3 * sizeof(double));
+    ALLOC(b->d_point, F * 3 * sizeof(double));
+    ALLOC(b->d_has_point, F);
+    ALLOC(b->d_xw, F * 3 * sizeof(double));
+    ALLOC(b->d_jimg, F * 12 * sizeof(double));
+    ALLOC(b->d_cuv, F * 2 * sizeof(double));
+    ALLOC(b->d_fvis, F);
+    ALLOC(b->d_res, F * area * sizeof(double));
+    ALLOC(b->d_pose_out, (size_t)n_pairs * 7 * sizeof(double));
+    ALLOC(b->d_err, (size_t)n_pairs * sizeof(double));
+    ALLOC(b->d_status, (size_t)n_pairs * sizeof(int32_t));
+    ALLOC(b->d_traces, (size_t)n_pairs * (prm->max_level + 1) * sizeof(svo_level_trace));
+#undef ALLOC
+    if (e != hipSuccess) {
+        free_batch(b);
+        delete b;
+        return fail(SVO_ERR_HIP, "hipMalloc(align batch): %s", hipGetErrorString(e));
+    }
+    *out = b;
+    return SVO_OK;
+}
+
+int svo_align_batch_destroy(svo_align_batch* b) {
+    if (!b) return SVO_OK;
+    (void)hipSetDevice(b->ctx->device);
+    (void)hipStreamSynchronize(b->ctx->stream);
+    free_batch(b);
+    delete b;
+    return SVO_OK;
+}
+
+static int check_frame(const svo_align_batch* b, const svo_pyramid_set* pyr, int32_t f) {
+    if (!pyr) return fail(SVO_ERR_ARG, "null pyramid set");
+    if (pyr->ctx != b->ctx) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
+    if (pyr->width != b->cam.width || pyr->height != b->cam.height || pyr->levels < b->params.max_level + 1)
+        return fail(SVO_ERR_ARG, "pyramid geometry %dx%d/%d does not match camera %dx%d / max_level %d", pyr->width,
+                    pyr->height, pyr->levels, b->cam.width, b->cam.height, b->params.max_level);
+    if (f < 0 || f >= pyr->n_frames) return fail(SVO_ERR_ARG, "frame index %d out of range", f);
+    return SVO_OK;
+}
+
+int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid_set* ref_set, int32_t ref_frame,
+                             const svo_pyramid_set* kf_set, int32_t kf_frame, const svo_pyramid_set* cur_set,
+                             int32_t cur_frame, const double* ref_pose, const double* kf_pose,
+                             const double* cur_pose, int32_t n_ref, int32_t n_kf, const double* px,
+                             const double* bearing, const double* point, const uint8_t* has_point) {
+    if (!b || !ref_pose || !kf_pose || !cur_pose) return fail(SVO_ERR_ARG, "null argument");
+    if (pair < 0 || pair >= b->n_pairs) return fail(SVO_ERR_ARG, "pair %d out of range", pair);
+    if (n_ref < 0 || n_kf < 0 || n_ref + n_kf > b->max_f)
+        return fail(SVO_ERR_ARG, "n_ref+n_kf = %d exceeds max_features %d", n_ref + n_kf, b->max_f);
+    const int32_t nf = n_ref + n_kf;
+    if (nf > 0 && (!px || !bearing || !point || !has_point)) return fail(SVO_ERR_ARG, "null feature array");
+    int rc;
+    if ((rc = check_frame(b, ref_set, ref_frame)) != SVO_OK) return rc;
+    if ((rc = check_frame(b, kf_set, kf_frame)) != SVO_OK) return rc;
+    if ((rc = check_frame(b, cur_set, cur_frame)) != SVO_OK) return rc;
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    svo::PairDesc& d = b->h_pairs[pair];
+    d.ref_pyr = ref_set->d_base + (size_t)ref_frame * ref_set->stride;
+    d.kf_pyr = kf_set->d_base + (size_t)kf_frame * kf_set->stride;
+    d.cur_pyr = cur_set->d_base + (size_t)cur_frame * cur_set->stride;
+    std::memcpy(d.ref_pose, ref_pose, 7 * sizeof(double));
+    std::memcpy(d.kf_pose, kf_pose, 7 * sizeof(double));
+    std::memcpy(d.cur_pose, cur_pose, 7 * sizeof(double));
+    d.n_ref = n_ref;
+    d.n_kf = n_kf;
+    const size_t fo = (size_t)pair * b->max_f;
+    hipStream_t s = b->ctx->stream;
+    if (nf > 0) {
+        SVO_HIP(hipMemcpyAsync(b->d_px + 2 * fo, px, nf * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+        SVO_HIP(hipMemcpyAsync(b->d_bearing + 3 * fo, bearing, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+        SVO_HIP(hipMemcpyAsync(b->d_point + 3 * fo, point, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+        SVO_HIP(hipMemcpyAsync(b->d_has_point + fo, has_point, nf, hipMemcpyHostToDevice, s));
+    }
+    SVO_HIP(hipMemcpyAsync(b->d_pairs + pair, &d, sizeof(d), hipMemcpyHostToDevice, s));
+    SVO_HIP(hipStreamSynchronize(s));
+    b->pair_set[pair] = 1;
+    return SVO_OK;
+}
+
+int svo_align_batch_set_initial_poses(svo_align_batch* b, const double* poses) {
+    if (!b || !poses) return fail(SVO_ERR_ARG, "null argument");
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    for (int32_t i = 0; i < b->n_pairs; ++i) std::memcpy(b->h_pairs[i].cur_pose, poses + 7 * i, 7 * sizeof(double));
+    SVO_HIP(hipMemcpyAsync(b->d_pairs, b->h_pairs.data(), sizeof(svo::PairDesc) * b->n_pairs, hipMemcpyHostToDevice,
+                           b->ctx->stream));
+    SVO_HIP(hipStreamSynchronize(b->ctx->stream));
+    return SVO_OK;
+}
+
+int svo_align_batch_run(svo_align_batch* b) {
+    if (!b) return fail(SVO_ERR_ARG, "null argument");
+    for (int32_t i = 0; i < b->n_pairs; ++i)
+        if (!b->pair_set[i]) return fail(SVO_ERR_STATE, "pair %d was never set", i);
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    svo::AlignArgs a;
+    a.pairs = b->d_pairs;
+    a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
+    a.xw = b->d_xw; a.jimg = b->d_jimg; a.cuv = b->d_cuv; a.fvis = b->d_fvis; a.res = b->d_res;
+    a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
+    a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
+    a.min_level = b->params.min_level; a.max_level = b->params.max_level;
+    a.fx = b->cam.fx; a.fy = b->cam.fy; a.cx = b->cam.cx; a.cy = b->cam.cy;
+    a.geom = b->geom;
+    svo::launch_align(a, b->ctx->stream);
+    SVO_HIP(hipGetLastError());
+    b->ran = true;
+    return SVO_OK;
+}
+
+int svo_align_batch_results(svo_align_batch* b, double* poses, double* err, int32_t* status) {
+    if (!b) return fail(SVO_ERR_ARG, "null argument");
+    if (!b->ran) return fail(SVO_ERR_STATE, "batch has not been run");
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    hipStream_t s = b->ctx->stream;
+    if (poses) SVO_HIP(hipMemcpyAsync(poses, b->d_pose_out, (size_t)b->n_pairs * 7 * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (err) SVO_HIP(hipMemcpyAsync(err, b->d_err, (size_t)b->n_pairs * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (status) SVO_HIP(hipMemcpyAsync(status, b->d_status, (size_t)b->n_pairs * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    SVO_HIP(hipStreamSynchronize(s));
+    return SVO_OK;
+}
+
+int svo_align_batch_traces(svo_align_batch* b, int32_t pair, svo_level_trace* out) {
+    if (!b || !out) return fail(SVO_ERR_ARG, "null argument");
+    if (!b->ran) return fail(SVO_ERR_STATE, "batch has not been run");
+    if (pair < 0 || pair >= b->n_pairs) return fail(SVO_ERR_ARG, "pair out of range");
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    const int L = b->params.max_level + 1;
+    SVO_HIP(hipMemcpyAsync(out, b->d_traces + (size_t)pair * L, L * sizeof(svo_level_trace), hipMemcpyDeviceToHost,
+                           b->ctx->stream));
+    SVO_HIP(hipStreamSynchronize(b->ctx->stream));
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ feature alignment
+int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, const svo_pyramid_set* ref_set,
+                      const int32_t* ref_frames, int32_t ref_frame, const svo_pyramid_set* cur_set, int32_t cur_frame,
+                      int32_t n, const double* ref_px, double* px_inout, double* err, int32_t* status) {
+    if (!c || !cam || !ref_set || !cur_set || (n > 0 && (!ref_px || !px_inout))) return fail(SVO_ERR_ARG, "null argument");
+    if (n < 0) return fail(SVO_ERR_ARG, "n < 0");
+    if (patch_size < 1 || (2 * (patch_size / 2) + 1) * (2 * (patch_size / 2) + 1) > 128)
+        return fail(SVO_ERR_ARG, "patch_size %d unsupported (footprint must be <= 128 px)", patch_size);
+    for (const svo_pyramid_set* p : {ref_set, cur_set}) {
+        if (p->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
+        if (p->width != cam->width || p->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
+    }
+    if (cur_frame < 0 || cur_frame >= cur_set->n_frames) return fail(SVO_ERR_ARG, "cur_frame out of range");
+    if (n == 0) return SVO_OK;
+    std::vector<const uint8_t*> rg(n);
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t f = ref_frames ? ref_frames[i] : ref_frame;
+        if (f < 0 || f >= ref_set->n_frames) return fail(SVO_ERR_ARG, "ref frame %d out of range", f);
+        rg[i] = ref_set->d_base + (size_t)f * ref_set->stride + ref_set->grad_off;
+    }
+    SVO_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint8_t** d_rg = nullptr;
+    int32_t* d_st = nullptr;
+    double *d_rpx = nullptr, *d_px = nullptr, *d_err = nullptr;
+    hipError_t e = hipMalloc(&d_rg, n * sizeof(void*));
+    if (e == hipSuccess) e = hipMalloc(&d_st, n * sizeof(int32_t));
+    if (e == hipSuccess) e = hipMalloc(&d_rpx, n * 2 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&d_px, n * 2 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc(&d_err, n * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpyAsync(d_rg, rg.data(), n * sizeof(void*), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_rpx, ref_px, n * 2 * sizeof(double), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_px, px_inout, n * 2 * sizeof(double), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        svo::FeatureAlignArgs a;
+        a.ref_grad = d_rg;
+        a.cur_grad = cur_set->d_base + (size_t)cur_frame * cur_set->stride + cur_set->grad_off;
+        a.ref_px = d_rpx;
+        a.px = d_px;
+        a.err = d_err;
+        a.status = d_st;
+        a.n = n;
+        a.half = patch_size / 2;
+        a.area = (2 * a.half + 1) * (2 * a.half + 1);
+        a.width = cam->width;
+        a.height = cam->height;
+        svo::launch_feature_align(a, s);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(px_inout, d_px, n * 2 * sizeof(double), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && err) e = hipMemcpyAsync(err, d_err, n * sizeof(double), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && status) e = hipMemcpyAsync(status, d_st, n * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    for (void* p : {(void*)d_rg, (void*)d_st, (void*)d_rpx, (void*)d_px, (void*)d_err})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
+    return SVO_OK;
+}
+
+}  // extern "C"

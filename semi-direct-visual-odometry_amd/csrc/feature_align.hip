@@ -1,0 +1,163 @@
+// feature_align.hip — FeatureAlignment::align (src/feature_alignment.cpp:25-62) for a batch of candidates.
+//
+// One 64-lane wave per candidate: the (2h+1)^2 patch (49 px at the reference's patch 7, src/map.cpp:18)
+// maps onto the wave's lanes.  Everything a lane computes is the reference's per-pixel arithmetic on the
+// level-0 GRADIENT images (float-rounded bilinear, src/algorithm.cpp:885-894); the order statistics for
+// the Tukey scale are exact ranks over the wave (the patch area is odd, so the reference's median is an
+// exact order statistic too); chi2, J^T W J and J^T W r are then summed by lane 0 in row order, the
+// reference's own order (src/optimizer.cpp:279-280), so the 3x3 system is bit-identical to the CPU
+// restatement.  Solve: Nielsen damping + Eigen-LDLT; update flow += dx (:200-205).
+#include "svo_internal.h"
+#include "svo_math.h"
+
+namespace svo {
+
+namespace {
+
+constexpr int kWavesPerBlock = 4;
+constexpr int kMaxArea = 128;
+
+struct WaveLds {
+    double r[kMaxArea];
+    double v[kMaxArea];
+    double w[kMaxArea];
+    double jx[kMaxArea];
+    double jy[kMaxArea];
+    double med;
+    double sel;
+};
+
+__device__ __forceinline__ bool in_frame(double x, double y, double b, int W, int H) {  // src/pinhole_camera.cpp:163-168
+    return x >= b && y >= b && x < W - b && y < H - b;
+}
+
+// k-th smallest (0-based) of v[0..m) held in LDS; every lane returns it
+__device__ double wave_kth(WaveLds& L, int m, int k) {
+    const int lane = threadIdx.x & 63;
+    for (int i = lane; i < m; i += 64) {
+        const double vi = L.v[i];
+        int rank = 0;
+        for (int j = 0; j < m; ++j) {
+            const double vj = L.v[j];
+            rank += (vj < vi) | ((vj == vi) & (j < i));
+        }
+        if (rank == k) L.sel = vi;
+    }
+    __syncthreads();
+    const double s = L.sel;
+    __syncthreads();
+    return s;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64 * kWavesPerBlock) feature_align_kernel(FeatureAlignArgs a) {
+    __shared__ WaveLds lds[kWavesPerBlock];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * kWavesPerBlock + wv;
+    WaveLds& L = lds[wv];
+    const bool active = i < a.n;  // whole waves are active or not; all waves still reach every barrier
+    const int A = a.area, h = a.half, side = 2 * a.half + 1;
+    const int W = a.width, H = a.height;
+    const double border = h + 2;
+    const double DMAX = 1.7976931348623157e308;
+
+    const uint8_t* gref = nullptr;
+    const uint8_t* gcur = a.cur_grad;
+    double rx = 0, ry = 0, fx = 0, fy = 0;
+    if (active) {
+        gref = a.ref_grad[i];
+        rx = a.ref_px[2 * i]; ry = a.ref_px[2 * i + 1];
+        fx = a.px[2 * i]; fy = a.px[2 * i + 1];
+    }
+    const bool ref_in = active && in_frame(rx, ry, border, W, H);
+    const bool cur_in = active && in_frame(fx, fy, border, W, H);
+    const int n = cur_in ? A : 0;
+
+    // computeJacobian (:64-110) + computeResiduals (:113-168)
+    for (int k = lane; k < A; k += 64) {
+        const int ky = k / side - h, kx = k - (k / side) * side - h;
+        double T = 0.0, jx = 0.0, jy = 0.0;
+        if (ref_in) {
+            const double row = ry + ky, col = rx + kx;
+            T = (double)bilinear_f(gref, W, col, row);
+            jx = 0.5 * (bilinear_f(gref, W, col + 1, row) - bilinear_f(gref, W, col - 1, row));
+            jy = 0.5 * (bilinear_f(gref, W, col, row + 1) - bilinear_f(gref, W, col, row - 1));
+        }
+        double r = DMAX;
+        if (cur_in) {
+            const double cur = (double)bilinear_f(gcur, W, fx + kx, fy + ky);
+            r = -(cur - T + 0.0);
+        }
+        L.r[k] = r;
+        L.v[k] = r;
+        L.jx[k] = jx;
+        L.jy[k] = jy;
+    }
+    __syncthreads();
+    // tukeyWeighting -> computeSigma(r, n) with the full-length vector (A entries, A odd)
+    const int mid = n / 2;
+    const double med = wave_kth(L, A, mid);
+    for (int k = lane; k < A; k += 64) L.v[k] = fabs(L.r[k] - med);
+    __syncthreads();
+    const double mad = wave_kth(L, A, mid);
+    double sigma = 1.482602218505602 * mad;
+    if (sigma <= 2.220446049250313e-16) sigma = 2.220446049250313e-16;
+    const double c = 4.6851 * sigma, c2 = c * c;
+    for (int k = lane; k < A; k += 64) {
+        double w = 0.0;
+        if (cur_in) {
+            const double r = L.r[k];
+            if (fabs(r) <= c) {
+                const double t = 1.0 - (r * r) / c2;
+                w = t * t;
+            }
+        }
+        L.w[k] = w;
+    }
+    __syncthreads();
+    if (active && lane == 0) {
+        double chi = 0.0, Hm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+        for (int k = 0; k < A; ++k) {
+            if (!cur_in) break;
+            const double r = L.r[k], w = L.w[k];
+            chi += r * r * w;
+            if (w == 0.0) continue;
+            const double J[3] = {L.jx[k], L.jy[k], ref_in ? 1.0 : 0.0};
+            for (int p = 0; p < 3; ++p) {
+                const double jw = J[p] * w;
+                for (int q = 0; q < 3; ++q) Hm[p * 3 + q] += jw * J[q];
+                g[p] += jw * r;
+            }
+        }
+        double mx = Hm[0];
+        mx = fmax(mx, Hm[4]);
+        mx = fmax(mx, Hm[8]);
+        const double lambda = 1e-2 * mx;
+        for (int p = 0; p < 3; ++p) Hm[p * 4] += lambda;
+        double dx[3];
+        ldlt_solve(3, Hm, g, dx);
+        const double nx = fx + dx[0], ny = fy + dx[1];
+        bool big = false, nan = false;
+        for (int p = 0; p < 3; ++p) { big |= dx[p] > 1e3; nan |= isnan(dx[p]); }
+        int32_t st = kSuccess;
+        if (big) st = kMaxCoffDx;
+        else if (nan) st = kNonInDx;
+        else {
+            const double step = dx[0] * dx[0] + dx[1] * dx[1] + dx[2] * dx[2];
+            st = step < 1e-16 ? kSmallStepSize : st;
+            st = fabs(lambda) >= 1e14 ? kLambdaValue : st;
+        }
+        a.px[2 * i] = nx;
+        a.px[2 * i + 1] = ny;
+        a.err[i] = sqrt(chi / (double)n);
+        a.status[i] = st;
+    }
+}
+
+void launch_feature_align(const FeatureAlignArgs& a, hipStream_t s) {
+    const int blocks = (a.n + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks > 0) hipLaunchKernelGGL(feature_align_kernel, dim3(blocks), dim3(64 * kWavesPerBlock), 0, s, a);
+}
+
+}  // namespace svo

@@ -1,0 +1,126 @@
+// svo.cpp — implementation of the C++ class-surface mirror (host/svo.hpp) over the C ABI.
+#include "svo.hpp"
+
+#include <cmath>
+#include <string>
+
+namespace svo_amd {
+
+static void check(int rc) {
+    if (rc != SVO_OK) throw Error(rc, std::string("svo: ") + svo_last_error());
+}
+
+Context::Context(int device) { check(svo_ctx_create(device, &m_ctx)); }
+Context::~Context() { svo_ctx_destroy(m_ctx); }
+
+Vec2 PinholeCamera::project2d(const Vec3& p) const { return {fx * (p[0] / p[2]) + cx, fy * (p[1] / p[2]) + cy}; }
+Vec3 PinholeCamera::inverseProject2d(const Vec2& px) const {
+    Vec3 v{(px[0] - cx) / fx, (px[1] - cy) / fy, 1.0};
+    const double n = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    return {v[0] * (1.0 / n), v[1] * (1.0 / n), v[2] * (1.0 / n)};
+}
+bool PinholeCamera::isInFrame(const Vec2& p, double b) const {
+    return p[0] >= b && p[1] >= b && p[0] < width - b && p[1] < height - b;
+}
+
+ImagePyramid::ImagePyramid(Context& ctx, std::size_t levels) : m_ctx(ctx), m_levels(levels) {}
+ImagePyramid::ImagePyramid(Context& ctx, const uint8_t* img, int32_t w, int32_t h, std::size_t levels)
+    : m_ctx(ctx), m_levels(levels) {
+    createImagePyramid(img, w, h, levels);
+}
+ImagePyramid::~ImagePyramid() { clear(); }
+void ImagePyramid::createImagePyramid(const uint8_t* img, int32_t w, int32_t h, std::size_t levels) {
+    clear();
+    m_levels = levels;
+    check(svo_pyramid_set_create(m_ctx.get(), 1, w, h, (int32_t)levels, &m_set));
+    check(svo_pyramid_set_upload(m_set, 0, 1, img));
+    check(svo_pyramid_set_build(m_set, 0, 1));
+    check(svo_ctx_synchronize(m_ctx.get()));
+}
+std::array<int32_t, 2> ImagePyramid::getImageSizeAtLevel(std::size_t level) const {
+    std::array<int32_t, 2> s{0, 0};
+    if (m_set) check(svo_pyramid_level_size(m_set, (int32_t)level, &s[0], &s[1]));
+    return s;
+}
+std::vector<uint8_t> ImagePyramid::getImageAtLevel(std::size_t level) const {
+    auto s = getImageSizeAtLevel(level);
+    std::vector<uint8_t> out((size_t)s[0] * s[1]);
+    check(svo_pyramid_set_download(m_set, 0, (int32_t)level, 0, out.data()));
+    return out;
+}
+std::vector<uint8_t> ImagePyramid::getGradientAtLevel(std::size_t level) const {
+    auto s = getImageSizeAtLevel(level);
+    std::vector<uint8_t> out((size_t)s[0] * s[1]);
+    check(svo_pyramid_set_download(m_set, 0, (int32_t)level, 1, out.data()));
+    return out;
+}
+void ImagePyramid::clear() {
+    if (m_set) svo_pyramid_set_destroy(m_set);
+    m_set = nullptr;
+}
+
+Feature::Feature(Frame* frame, const Vec2& px)
+    : m_frame(frame), m_pixelPosition(px), m_bearingVec(frame->m_camera->inverseProject2d(px)) {}
+
+Frame::Frame(Context& ctx, std::shared_ptr<PinholeCamera> camera, const uint8_t* img, uint32_t maxImagePyramid,
+             std::shared_ptr<Frame> lastKeyframe)
+    : m_camera(std::move(camera)), m_imagePyramid(ctx, maxImagePyramid), m_lastKeyframe(std::move(lastKeyframe)) {
+    if (!img) throw std::runtime_error("Image Corrupted");  // src/frame.cpp:20-24
+    m_imagePyramid.createImagePyramid(img, m_camera->width, m_camera->height, maxImagePyramid);
+}
+
+ImageAlignment::ImageAlignment(Context& ctx, uint32_t patchSize, int32_t minLevel, int32_t maxLevel, uint32_t numParameters)
+    : m_ctx(ctx), m_params{(int32_t)patchSize, minLevel, maxLevel, 0} {
+    if (numParameters != 6) throw Error(SVO_ERR_ARG, "ImageAlignment: numParameters must be 6");
+}
+
+double ImageAlignment::align(std::shared_ptr<Frame>& refFrame, std::shared_ptr<Frame>& curFrame) {
+    if (refFrame->numberObservation() == 0) return 0;  // src/image_alignment.cpp:27-28
+    const auto& kf = refFrame->m_lastKeyframe;
+    const int32_t nr = (int32_t)refFrame->numberObservation(), nk = (int32_t)kf->numberObservation();
+    std::vector<double> px, br, pt;
+    std::vector<uint8_t> hp;
+    for (const auto* fr : {refFrame.get(), kf.get()})
+        for (const auto& f : fr->m_features) {
+            px.insert(px.end(), f->m_pixelPosition.begin(), f->m_pixelPosition.end());
+            br.insert(br.end(), f->m_bearingVec.begin(), f->m_bearingVec.end());
+            const Vec3 p = f->m_point ? f->m_point->m_position : Vec3{0, 0, 0};
+            pt.insert(pt.end(), p.begin(), p.end());
+            hp.push_back(f->m_point ? 1 : 0);
+        }
+    svo_camera cam = refFrame->m_camera->c();
+    svo_align_batch* b = nullptr;
+    check(svo_align_batch_create(m_ctx.get(), &cam, &m_params, 1, nr + nk, &b));
+    double err = 0.0;
+    try {
+        check(svo_align_batch_set_pair(b, 0, refFrame->m_imagePyramid.set(), 0, kf->m_imagePyramid.set(), 0,
+                                       curFrame->m_imagePyramid.set(), 0, refFrame->m_absPose.data(),
+                                       kf->m_absPose.data(), curFrame->m_absPose.data(), nr, nk, px.data(), br.data(),
+                                       pt.data(), hp.data()));
+        check(svo_align_batch_run(b));
+        check(svo_align_batch_results(b, curFrame->m_absPose.data(), &err, &m_status));
+    } catch (...) {
+        svo_align_batch_destroy(b);
+        throw;
+    }
+    svo_align_batch_destroy(b);
+    return err;
+}
+
+FeatureAlignment::FeatureAlignment(Context& ctx, uint32_t patchSize, int32_t level, uint32_t numParameters)
+    : m_ctx(ctx), m_patchSize(patchSize) {
+    if (numParameters != 3) throw Error(SVO_ERR_ARG, "FeatureAlignment: numParameters must be 3");
+    if (level != 0) throw Error(SVO_ERR_ARG, "FeatureAlignment works on level 0 (src/feature_alignment.cpp:69)");
+}
+
+double FeatureAlignment::align(const std::shared_ptr<Feature>& refFeature, const std::shared_ptr<Frame>& curFrame,
+                               Vec2& pixelPos) {
+    svo_camera cam = curFrame->m_camera->c();
+    double err = 0.0;
+    check(svo_feature_align(m_ctx.get(), &cam, (int32_t)m_patchSize, refFeature->m_frame->m_imagePyramid.set(), nullptr,
+                            0, curFrame->m_imagePyramid.set(), 0, 1, refFeature->m_pixelPosition.data(),
+                            pixelPos.data(), &err, &m_status));
+    return err;
+}
+
+}  // namespace svo_amd

@@ -1,0 +1,125 @@
+// svo.hpp — C++ mirror of the reference's alignment class surface over the C ABI (include/svo_c.h).
+//
+// The reference's callers (src/system.cpp:313, src/map.cpp:538,608, src/frame.cpp:26) use
+//   ImageAlignment(patchSize, minLevel, maxLevel, numParameters); double align(ref, cur);
+//   FeatureAlignment(patchSize, level, numParameters);            double align(feature, cur, pixelPos);
+//   ImagePyramid(baseImage, maxPyramidLevel) + getters.
+// The same names, argument meaning and error behaviour are kept here over self-contained types
+// (Eigen / Sophus / OpenCV are absent from this image; INTEGRATION.md shows the adapter a maintainer adds
+// to feed cv::Mat / Sophus::SE3d / Eigen::Vector2d through these types unchanged).
+#pragma once
+#include <array>
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <vector>
+
+#include "svo_c.h"
+
+namespace svo_amd {
+
+using Pose = std::array<double, 7>;  // Sophus::SE3d::params(): qx qy qz qw tx ty tz
+using Vec2 = std::array<double, 2>;
+using Vec3 = std::array<double, 3>;
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const std::string& msg) : std::runtime_error(msg), code(code) {}
+    int code;
+};
+
+class Context {
+public:
+    explicit Context(int device = 0);
+    ~Context();
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    svo_ctx* get() const { return m_ctx; }
+
+private:
+    svo_ctx* m_ctx = nullptr;
+};
+
+struct PinholeCamera {  // include/pinhole_camera.hpp:16 (undistorted)
+    int32_t width, height;
+    double fx, fy, cx, cy;
+    Vec2 project2d(const Vec3& p) const;
+    Vec3 inverseProject2d(const Vec2& px) const;
+    bool isInFrame(const Vec2& p, double boundary = 0.0) const;
+    svo_camera c() const { return {fx, fy, cx, cy, width, height}; }
+};
+
+// ImagePyramid (include/image_pyramid.hpp:23-149): device resident; copy/move deleted like the reference.
+class ImagePyramid {
+public:
+    ImagePyramid(Context& ctx, std::size_t maxPyramidLevel);
+    ImagePyramid(Context& ctx, const uint8_t* baseImage, int32_t width, int32_t height, std::size_t maxPyramidLevel);
+    ImagePyramid(const ImagePyramid&) = delete;
+    ImagePyramid& operator=(const ImagePyramid&) = delete;
+    ~ImagePyramid();
+    void createImagePyramid(const uint8_t* baseImage, int32_t width, int32_t height, std::size_t maxPyramidLevel);
+    std::vector<uint8_t> getImageAtLevel(std::size_t level) const;
+    std::vector<uint8_t> getGradientAtLevel(std::size_t level) const;
+    std::vector<uint8_t> getBaseImage() const { return getImageAtLevel(0); }
+    std::vector<uint8_t> getBaseGradientImage() const { return getGradientAtLevel(0); }
+    std::size_t getSizeImagePyramid() const { return m_set ? m_levels : 0; }
+    std::array<int32_t, 2> getImageSizeAtLevel(std::size_t level) const;  // (width, height); (0,0) past the top
+    std::array<int32_t, 2> getBaseImageSize() const { return getImageSizeAtLevel(0); }
+    void clear();
+    const svo_pyramid_set* set() const { return m_set; }
+
+private:
+    Context& m_ctx;
+    svo_pyramid_set* m_set = nullptr;
+    std::size_t m_levels;
+};
+
+struct Frame;
+struct Point {
+    Vec3 m_position;
+};
+struct Feature {  // include/feature.hpp:14
+    Frame* m_frame;
+    Vec2 m_pixelPosition;
+    Vec3 m_bearingVec;
+    std::shared_ptr<Point> m_point;
+    Feature(Frame* frame, const Vec2& px);
+};
+struct Frame {  // include/frame.hpp:70-208 (the members the alignment path reads)
+    Frame(Context& ctx, std::shared_ptr<PinholeCamera> camera, const uint8_t* img, uint32_t maxImagePyramid,
+          std::shared_ptr<Frame> lastKeyframe = nullptr);
+    std::shared_ptr<PinholeCamera> m_camera;
+    Pose m_absPose{0, 0, 0, 1, 0, 0, 0};
+    ImagePyramid m_imagePyramid;
+    std::vector<std::shared_ptr<Feature>> m_features;
+    std::shared_ptr<Frame> m_lastKeyframe;
+    std::size_t numberObservation() const { return m_features.size(); }
+};
+
+// ImageAlignment (include/image_alignment.hpp:15-73)
+class ImageAlignment {
+public:
+    ImageAlignment(Context& ctx, uint32_t patchSize, int32_t minLevel, int32_t maxLevel, uint32_t numParameters);
+    double align(std::shared_ptr<Frame>& refFrame, std::shared_ptr<Frame>& curFrame);
+    int32_t lastStatus() const { return m_status; }
+
+private:
+    Context& m_ctx;
+    svo_align_params m_params;
+    int32_t m_status = SVO_STATUS_FAILED;
+};
+
+// FeatureAlignment (include/feature_alignment.hpp:15-43)
+class FeatureAlignment {
+public:
+    FeatureAlignment(Context& ctx, uint32_t patchSize, int32_t level, uint32_t numParameters);
+    double align(const std::shared_ptr<Feature>& refFeature, const std::shared_ptr<Frame>& curFrame, Vec2& pixelPos);
+    int32_t lastStatus() const { return m_status; }
+
+private:
+    Context& m_ctx;
+    uint32_t m_patchSize;
+    int32_t m_status = SVO_STATUS_FAILED;
+};
+
+}  // namespace svo_amd

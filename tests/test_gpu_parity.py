@@ -1,0 +1,185 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on the same inputs.
+
+Tolerances:
+  * pyramid / gradient levels, visibility and pixel counts ....... bit-exact
+  * Tukey scale (median, MAD, sigma) ............................. bit-exact (exact-order-statistic oracle)
+  * H, g (summation order differs) ................................ 1e-10 relative to max |entry|
+  * final pose vs the exact-statistic oracle ....................... 1e-9 (Sophus params, sign-canonical)
+  * final pose vs the reference semantics (libstdc++ nth_element) .. 1e-5 (north_star tolerance)
+  * FeatureAlignment (px, err, status) ........................... bit-exact
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import svo_amd
+import svo_amd.synth as synth
+from common import canon, gpu_batch, make_pairs, oracle_align
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pairs4():
+    return make_pairs(4)
+
+
+def test_pyramid_bitexact():
+    rng = np.random.default_rng(7)
+    s = synth.make_pair()
+    for (h, w, lv) in [(376, 1241, 5), (37, 101, 4), (64, 64, 3), (5, 7, 2)]:
+        imgs = [rng.integers(0, 256, (h, w), dtype=np.uint8) for _ in range(2)]
+        if (h, w) == (376, 1241):
+            imgs = [s.ref_img, s.cur_img] + imgs
+        ps = svo_amd.PyramidSet(len(imgs), w, h, lv)
+        ps.upload(0, np.stack(imgs))
+        ps.build()
+        for i, im in enumerate(imgs):
+            oi, og = O.build_pyramid(im, lv)
+            li, lg = O.unpack_levels(oi, w, h, lv), O.unpack_levels(og, w, h, lv)
+            for l in range(lv):
+                assert np.array_equal(ps.download(i, l, False), li[l]), (h, w, i, l, "image")
+                assert np.array_equal(ps.download(i, l, True), lg[l]), (h, w, i, l, "gradient")
+
+
+def _check_traces(tr_gpu, tr_cpu, min_level, max_level, exact_levels):
+    for l in range(max_level, min_level - 1, -1):
+        g, c = tr_gpu[l], tr_cpu[l]
+        assert (g.n_ref_vis, g.n_vis, g.status) == (c.n_ref_vis, c.n_vis, c.status), (l, g.n_vis, c.n_vis)
+        if l in exact_levels:
+            assert g.median == c.median and g.mad == c.mad and g.sigma == c.sigma, l
+        else:
+            assert abs(g.sigma - c.sigma) <= 1e-9 * abs(c.sigma), l
+        Hg = np.tril(np.array(g.H).reshape(6, 6))
+        Hc = np.tril(np.array(c.H).reshape(6, 6))
+        assert np.abs(Hg - Hc).max() <= 1e-10 * np.abs(Hc).max(), l
+        gg, gc = np.array(g.g), np.array(c.g)
+        assert np.abs(gg - gc).max() <= 1e-9 * max(np.abs(gc).max(), 1e-300), l
+        assert abs(g.chi2 - c.chi2) <= 1e-10 * c.chi2, l
+
+
+@pytest.mark.parametrize("cfg", [dict(patch=5, min_level=0, max_level=4, nf=2000),   # config 2
+                                 dict(patch=4, min_level=0, max_level=2, nf=200),    # config 1 (5x5 footprint)
+                                 dict(patch=7, min_level=1, max_level=3, nf=600)])
+def test_align_matches_exact_oracle(cfg):
+    pairs = make_pairs(3, n_features=cfg["nf"], patch_size=cfg["patch"])
+    b, ps = gpu_batch(pairs, cfg["patch"], cfg["min_level"], cfg["max_level"])
+    b.run()
+    poses, err, st = b.results()
+    for i, s in enumerate(pairs):
+        pose_c, err_c, st_c, tr_c = oracle_align(s, cfg["patch"], cfg["min_level"], cfg["max_level"], mode=1)
+        _check_traces(b.traces(i), tr_c, cfg["min_level"], cfg["max_level"], exact_levels={cfg["max_level"]})
+        assert np.abs(canon(poses[i]) - canon(pose_c)).max() <= 1e-9
+        assert abs(err[i] - err_c) <= 1e-9 * abs(err_c)
+        assert st[i] == st_c
+
+
+def test_align_reference_semantics_pose_tolerance(pairs4):
+    b, ps = gpu_batch(pairs4, 5, 0, 4)
+    b.run()
+    poses, err, st = b.results()
+    for i, s in enumerate(pairs4):
+        pose_ref, err_ref, st_ref, _ = oracle_align(s, 5, 0, 4, mode=0, trace=False)
+        assert np.abs(canon(poses[i]) - canon(pose_ref)).max() <= 1e-5
+        assert abs(err[i] - err_ref) <= 1e-4 * err_ref
+        assert st[i] == st_ref
+
+
+def test_batch_composition_and_repeat_invariance(pairs4):
+    b, _ = gpu_batch(pairs4, 5, 0, 4)
+    b.run()
+    p_all, e_all, s_all = b.results()
+    b.run()
+    p_again, e_again, _ = b.results()
+    assert np.array_equal(p_all, p_again) and np.array_equal(e_all, e_again)
+    b1, _ = gpu_batch(pairs4[2:3], 5, 0, 4)
+    b1.run()
+    p1, e1, s1 = b1.results()
+    assert np.array_equal(p1[0], p_all[2]) and np.array_equal(e1[0], e_all[2]) and s1[0] == s_all[2]
+
+
+def test_align_edge_cases():
+    s = synth.make_pair(n_features=100, null_point_fraction=0.3)
+    # null-point features keep their slots (src/image_alignment.cpp:85-99)
+    b, _ = gpu_batch([s], 5, 0, 2)
+    b.run()
+    p, e, st = b.results()
+    pc, ec, stc, trc = oracle_align(s, 5, 0, 2, mode=1)
+    assert np.abs(canon(p[0]) - canon(pc)).max() <= 1e-9 and st[0] == stc
+    _check_traces(b.traces(0), trc, 0, 2, exact_levels={2})
+    # every feature without a point: nothing visible -> NaN error, Small_Step_Size (dx = 0)
+    s2 = synth.make_pair(n_features=40)
+    s2.has_point[:] = 0
+    b, _ = gpu_batch([s2], 5, 0, 2)
+    b.run()
+    p, e, st = b.results()
+    pc, ec, stc, _ = oracle_align(s2, 5, 0, 2, mode=1)
+    assert np.isnan(e[0]) and np.isnan(ec) and st[0] == stc == 3
+    assert np.array_equal(canon(p[0]), canon(pc))
+    # initial pose far away: the patches leave the current image
+    s3 = synth.make_pair(n_features=60)
+    far = s3.cur_init_pose.copy()
+    far[4] += 50.0
+    s3.cur_init_pose = far
+    b, _ = gpu_batch([s3], 5, 0, 2)
+    b.run()
+    p, e, st = b.results()
+    pc, ec, stc, _ = oracle_align(s3, 5, 0, 2, mode=1)
+    assert st[0] == stc and (np.isnan(e[0]) == np.isnan(ec))
+    assert np.abs(canon(p[0]) - canon(pc)).max() <= 1e-9
+
+
+def test_align_no_ref_features():
+    s = synth.make_pair(n_features=40)
+    s.n_kf, s.n_ref = s.n_ref + s.n_kf, 0
+    b, _ = gpu_batch([s], 5, 0, 2)
+    b.run()
+    p, e, st = b.results()
+    assert e[0] == 0.0 and np.array_equal(p[0], s.cur_init_pose)  # align() returns 0 (src/image_alignment.cpp:27-28)
+
+
+def test_class_surface_align():
+    s = synth.make_pair(n_features=300)
+    cam = svo_amd.PinholeCamera.kitti()
+    kf = svo_amd.Frame(cam, s.kf_img, 5)
+    kf.abs_pose[:] = s.kf_pose
+    ref = svo_amd.Frame(cam, s.ref_img, 5, last_keyframe=kf)
+    ref.abs_pose[:] = s.ref_pose
+    cur = svo_amd.Frame(cam, s.cur_img, 5, last_keyframe=kf)
+    cur.abs_pose[:] = s.cur_init_pose
+    for i in range(len(s.px)):
+        fr = ref if i < s.n_ref else kf
+        f = svo_amd.Feature(fr, s.px[i], bearing=s.bearing[i], point=svo_amd.Point(s.point[i]))
+        fr.add_feature(f)
+    err = svo_amd.ImageAlignment(5, 0, 4).align(ref, cur)
+    pc, ec, stc, _ = oracle_align(s, 5, 0, 4, mode=1)
+    assert np.abs(canon(cur.abs_pose) - canon(pc)).max() <= 1e-9
+    assert abs(err - ec) <= 1e-9 * ec
+    # ImagePyramid getters (src/image_pyramid.cpp:54-124)
+    assert np.array_equal(ref.image_pyramid.get_base_image(), s.ref_img)
+    assert ref.image_pyramid.get_image_size_at_level(4) == (78, 24)
+    assert ref.image_pyramid.get_image_size_at_level(5) == (0, 0)
+
+
+@pytest.mark.parametrize("patch", [7, 8, 5])
+def test_feature_align_bitexact(patch):
+    s = synth.make_pair(n_features=2000, patch_size=patch)
+    rng = np.random.default_rng(patch)
+    ref_grad = O.build_pyramid(s.ref_img, 1)[1]
+    cur_grad = O.build_pyramid(s.cur_img, 1)[1]
+    n = 2000
+    ref_px = s.px[:n].copy()
+    init = ref_px + rng.uniform(-1.5, 1.5, ref_px.shape)
+    init[:5] = [[-3, 10], [2, 2], [1240.5, 100], [600, 375.9], [3.5, 3.5]]  # out-of-frame / border cases
+    px_c, err_c, st_c = O.feature_align(s.camera, patch, ref_grad, cur_grad, ref_px, init)
+    ps = svo_amd.PyramidSet(2, 1241, 376, 1)
+    ps.upload(0, np.stack([s.ref_img, s.cur_img]))
+    ps.build()
+    px_g = init.copy()
+    fa = svo_amd.FeatureAlignment(patch)
+    err_g, st_g = fa.align_batch(ps, 0, ps, 1, ref_px, px_g, svo_amd.PinholeCamera.kitti())
+    assert np.array_equal(px_g, px_c)
+    assert np.array_equal(st_g, st_c)
+    assert np.array_equal(np.isnan(err_g), np.isnan(err_c))
+    ok = ~np.isnan(err_c)
+    assert np.array_equal(err_g[ok], err_c[ok])

@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU-box runner: each GPU step under its own time limit; stops at the first crash/timeout
+# (exit >= 124), continues past ordinary test failures so the later measurements still run.
+# usage: tools/gpu_round.sh <step>...   steps: smoke tests bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+run() {
+    local name=$1 limit=$2; shift 2
+    echo "== $name: $*"
+    timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 25 "gpurun_out/$name.log"
+    if [ "$rc" -ge 124 ]; then echo "== stopping after $name (rc=$rc)"; exit "$rc"; fi
+}
+for step in "$@"; do
+    case "$step" in
+        smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+        quick) run quick 300 python3 tests/gpu_smoke.py ;;
+        tests) run tests 900 python3 -m pytest tests -q -m gpu -p no:cacheprovider ;;
+        bench) run bench 600 python3 bench.py ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu ;;
+        pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
+        *) echo "unknown step $step" ;;
+    esac
+done
