@@ -131,6 +131,13 @@ def ldlt_solve(H, b):
     return x
 
 
+def image_jac(p3, fx, fy):
+    p3 = np.ascontiguousarray(p3, dtype=np.float64)
+    out = np.zeros((2, 6))
+    lib().oracle_image_jac(_p(p3), ctypes.c_double(fx), ctypes.c_double(fy), _p(out))
+    return out
+
+
 def median(v, n_valid, mode=0):
     v = np.ascontiguousarray(v, dtype=np.float64)
     return lib().oracle_median(_p(v), len(v), n_valid, mode)

@@ -791,6 +791,14 @@ double oracle_image_align(const oc_camera* c, int32_t patch, int32_t min_level, 
 
 int32_t oracle_level_trace_size(void) { return (int32_t)sizeof(LevelTrace); }
 
+// ImageAlignment::computeImageJac (src/image_alignment.cpp:194-248): out = 2 x 6 row-major
+void oracle_image_jac(const double* p3, double fx, double fy, double* out12) {
+    double J[2][6];
+    ImageAlignment::image_jac(J, {p3[0], p3[1], p3[2]}, fx, fy);
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 6; ++j) out12[i * 6 + j] = J[i][j];
+}
+
 // Many independent alignments on nthreads host threads (one alignment per thread at a time, each
 // single-threaded like the reference's main-thread call).  Used for the multi-core CPU baseline.
 void oracle_image_align_batch(const oc_camera* c, int32_t patch, int32_t min_level, int32_t max_level, int32_t median_mode,
