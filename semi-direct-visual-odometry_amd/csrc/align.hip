@@ -1,19 +1,28 @@
 // align.hip — sparse image alignment (ImageAlignment::align, src/image_alignment.cpp:25-67) on gfx950.
 //
-// One 512-thread workgroup owns one frame pair for the whole coarse-to-fine call: pairs are independent
-// (SURVEY.md §8(e)), so no workgroup ever talks to another and the batch needs one launch.  Per level:
-//   P1  per feature : ref visibility (border rule :140-149), cur projection pose*X_w (:320-340),
-//                     image Jacobian at the WORLD point (:163, :194-248)
-//   P2  per pixel   : r = bilerp(I_cur) - bilerp(I_ref) (:359), +inf for invisible slots; first radix
-//                     digit of the median histogrammed in LDS on the fly
-//   P3  exact median of the visible residuals (radix select over order-preserving uint64 keys,
-//                     11-bit digits, LDS histograms, candidate gather once a bucket is small)
-//   P4  exact median of |r - median|  -> sigma = 1.482602218505602 * MAD   (src/algorithm.cpp:834-872)
-//   P5  per pixel   : Tukey weight (src/optimizer.cpp:485-514), chi2, J row = dx*Jimg0 + dy*Jimg1 with
-//                     dx, dy re-sampled from the ref image, lower-triangular J^T W J and J^T W r in
-//                     registers; wave shuffles + fixed-order LDS tree (deterministic, no atomics)
-//   P6  one lane    : Nielsen damping, Eigen-LDLT solve, pose <- pose * exp(-dx), status, RMSE
-//                     (src/optimizer.cpp:279-366, src/image_alignment.cpp:379)
+// One 512-thread workgroup owns one frame pair for the whole coarse-to-fine call.  Pairs are
+// independent: no workgroup talks to another, a batch is one launch, and with
+// <= 128 VGPRs and ~62 KB of LDS two pairs share a CU.  Per level:
+//   P1  thread / feature : ref visibility (border rule :140-149), projection pose*X_w into cur (:320-340),
+//                          image Jacobian at the WORLD point (:163, :194-248) -> per-feature scratch
+//   S1  lane group / feature (32 lanes for the 25 px of patch 5, 64 for patch 7): the feature's ref
+//                          window ((2h+5)^2 px) and cur window ((2h+3)^2 px) are staged in LDS with a
+//                          few byte loads, then every lane samples its pixel: r = I_cur - T_ref (:359);
+//                          r goes to a per-pair scratch row (+inf = invisible slot), its value bin to an
+//                          LDS histogram (4096 bins of 1/8 grey level)
+//   S2  exact median (src/algorithm.cpp:834-853): the histogram names the bin of rank n/2; one sweep
+//                          gathers that bin's values (plus the max below it) into LDS; exact rank there.
+//   S3/S4  the same for |r - median| -> MAD -> sigma = 1.482602218505602 * MAD (:855-872)
+//   S5  lane group / feature : Tukey weight (src/optimizer.cpp:485-514), chi2, dx/dy re-sampled from the
+//                          staged ref window; per feature the 5 sums S_xx S_xy S_yy S_xr S_yr (shuffles
+//                          inside the lane group) expand with the 2x6 image Jacobian into the lower
+//                          triangle of J^T W J and J^T W r (factorised J row = dx*Jimg0 + dy*Jimg1);
+//                          wave shuffles + fixed-order LDS tree -> deterministic, no atomics
+//   P6  one lane          : Nielsen damping, Eigen-LDLT (LDS workspace), pose <- pose * exp(-dx),
+//                          status, RMSE (src/optimizer.cpp:279-366, src/image_alignment.cpp:379)
+// Exact order statistics: values are binned by a monotone map, so the bin of rank k and its
+// population are exact; a bin with more than kCandCap values falls back to an 11-bit radix select
+// on order-preserving uint64 keys restricted to that bin.
 #include "svo_internal.h"
 #include "svo_math.h"
 
@@ -23,23 +32,29 @@ namespace {
 
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
-constexpr int kDigitBits = 11;
-constexpr int kBins = 1 << kDigitBits;
-constexpr int kCandCap = 1024;
+constexpr int kBins = 4096;
+constexpr double kBinScale = 8.0;  // bins per grey level
+constexpr int kCandCap = 4096;
+constexpr int kRankCap = 1024;     // <= this many candidates: rank counting, else bitonic sort
+constexpr int kWinBytes = 1024;    // per-wave staging buffer
+constexpr int kRadixBits = 11;
 
 struct Shared {
     uint32_t hist[kBins];
-    uint64_t cand[kCandCap];
-    double red[kWaves][32];
+    double cand[kCandCap];
+    uint8_t win[kWaves][kWinBytes];
+    double red[kWaves][30];
+    double accw[kWaves][28];  // per-wave J^T W J (21, lower) | J^T W r (6) | chi2, fixed accumulation order
+    double tot[28];
     uint32_t ired[kWaves][4];
     uint32_t scan[kThreads];
+    double A[36];
+    double tmp[6];
+    int32_t perm[6];
     SE3 pose;
-    // selection state
     uint64_t sel_prefix;
-    uint32_t sel_k, sel_cnt, sel_bits, cand_n;
-    double sel_value;
-    double med, mad;
-    int32_t done;  // alignment ended early (status set)
+    uint32_t sel_k, sel_cnt, sel_bits, sel_bin, cand_n;
+    double sel_hi, sel_lo;
 };
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -54,57 +69,59 @@ __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
     return v;
 }
+__device__ __forceinline__ void wave_lds_sync() {  // make this wave's LDS writes visible to its own lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
-// block-wide sums of up to 4 uint32 counters; result valid in every thread after return
-__device__ void block_sum_u4(Shared& sh, uint32_t v[4]) {
+// block-wide sums of 2 counters, valid in every thread
+__device__ void block_sum_u2(Shared& sh, uint32_t& a, uint32_t& b) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int i = 0; i < 4; ++i) v[i] = wave_sum_u(v[i]);
-    if (lane == 0)
-        for (int i = 0; i < 4; ++i) sh.ired[wave][i] = v[i];
+    a = wave_sum_u(a);
+    b = wave_sum_u(b);
+    if (lane == 0) { sh.ired[wave][0] = a; sh.ired[wave][1] = b; }
     __syncthreads();
-    for (int i = 0; i < 4; ++i) {
-        uint32_t s = 0;
-        for (int w = 0; w < kWaves; ++w) s += sh.ired[w][i];
-        v[i] = s;
-    }
+    a = 0; b = 0;
+    for (int w = 0; w < kWaves; ++w) { a += sh.ired[w][0]; b += sh.ired[w][1]; }
     __syncthreads();
 }
 
-// value of a residual slot for the current selection (median pass: r; MAD pass: |r - med|)
+// selection value of a residual slot: kMad ? |r - med| : r   (monotone bin map per mode)
 template <bool kMad>
-__device__ __forceinline__ double sel_val(double r, double med) {
-    return kMad ? fabs(r - med) : r;
+__device__ __forceinline__ double sel_val(double r, double med) { return kMad ? fabs(r - med) : r; }
+template <bool kMad>
+__device__ __forceinline__ int sel_bin(double v) {
+    const double t = kMad ? v * kBinScale : (v + 256.0) * kBinScale;
+    return t < 0.0 ? 0 : (t >= (double)(kBins - 1) ? kBins - 1 : (int)t);
 }
 
-// Find the bucket holding rank sh.sel_k in sh.hist; updates prefix/k/cnt.  All threads call.
-__device__ void select_bucket(Shared& sh, int digit_bits) {
+// bin holding rank sh.sel_k of sh.hist -> sh.sel_bin, sh.sel_k (rank inside the bin), sh.sel_cnt
+__device__ void find_bin(Shared& sh, const uint32_t* hist, int bins) {
     const int tid = threadIdx.x;
-    const uint32_t k = sh.sel_k;  // read before any thread can update it (the scan below syncs)
-    const int bins = 1 << digit_bits;
+    const uint32_t k = sh.sel_k;
     const int per = (bins + kThreads - 1) / kThreads;
     uint32_t local = 0;
     for (int i = 0; i < per; ++i) {
         const int b = tid * per + i;
-        if (b < bins) local += sh.hist[b];
+        if (b < bins) local += hist[b];
     }
     sh.scan[tid] = local;
     __syncthreads();
-    // inclusive scan (Hillis-Steele on 512 entries)
     for (int o = 1; o < kThreads; o <<= 1) {
         const uint32_t add = tid >= o ? sh.scan[tid - o] : 0;
         __syncthreads();
         sh.scan[tid] += add;
         __syncthreads();
     }
-    const uint32_t incl = sh.scan[tid];
-    const uint32_t excl = incl - local;
+    const uint32_t incl = sh.scan[tid], excl = incl - local;
     if (k >= excl && k < incl) {
         uint32_t run = excl;
         for (int i = 0; i < per; ++i) {
             const int b = tid * per + i;
-            const uint32_t c = (b < bins) ? sh.hist[b] : 0;
+            const uint32_t c = b < bins ? hist[b] : 0;
             if (k < run + c) {
-                sh.sel_prefix = (sh.sel_prefix << digit_bits) | (uint64_t)b;
+                sh.sel_bin = (uint32_t)b;
                 sh.sel_k = k - run;
                 sh.sel_cnt = c;
                 break;
@@ -113,75 +130,84 @@ __device__ void select_bucket(Shared& sh, int digit_bits) {
         }
     }
     __syncthreads();
-    if (tid == 0) sh.sel_bits += digit_bits;
+}
+
+// k-th and (k-1)-th smallest of cand[0..n) (k-1 only if want_lo and k > 0)
+__device__ void cand_select(Shared& sh, uint32_t n, uint32_t kk, bool want_lo) {
+    const int tid = threadIdx.x;
+    if (n <= (uint32_t)kRankCap) {
+        for (uint32_t i = tid; i < n; i += kThreads) {
+            const double vi = sh.cand[i];
+            uint32_t rank = 0;
+            for (uint32_t j = 0; j < n; ++j) {
+                const double vj = sh.cand[j];
+                rank += (vj < vi) | ((vj == vi) & (j < i));
+            }
+            if (rank == kk) sh.sel_hi = vi;
+            if (want_lo && rank + 1 == kk) sh.sel_lo = vi;
+        }
+        __syncthreads();
+        return;
+    }
+    uint32_t p2 = 1;
+    while (p2 < n) p2 <<= 1;
+    for (uint32_t i = n + tid; i < p2; i += kThreads) sh.cand[i] = __builtin_inf();
+    __syncthreads();
+    for (uint32_t size = 2; size <= p2; size <<= 1)
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t i = tid; i < p2 / 2; i += kThreads) {
+                const uint32_t lo = (i / stride) * stride * 2 + (i % stride), hi = lo + stride;
+                const bool asc = (lo & size) == 0;
+                const double a = sh.cand[lo], b = sh.cand[hi];
+                if ((a > b) == asc) { sh.cand[lo] = b; sh.cand[hi] = a; }
+            }
+            __syncthreads();
+        }
+    if (tid == 0) {
+        sh.sel_hi = sh.cand[kk];
+        if (want_lo && kk > 0) sh.sel_lo = sh.cand[kk - 1];
+    }
     __syncthreads();
 }
 
-// Exact k-th smallest (0-based) of the visible slot values.  hist must already hold the first-digit
-// histogram (11 top bits of the key).  Returns the value in every thread.
+// radix fallback inside one overfull bin: exact k-th among values v with sel_bin(v) == bin
 template <bool kMad>
-__device__ double block_select(Shared& sh, const double* __restrict__ res, int M, uint32_t k, double med) {
+__device__ double radix_in_bin(Shared& sh, const double* __restrict__ res, int M, uint32_t bin, uint32_t k, double med) {
     const int tid = threadIdx.x;
-    if (tid == 0) { sh.sel_prefix = 0; sh.sel_k = k; sh.sel_bits = 0; sh.cand_n = 0; }
+    if (tid == 0) { sh.sel_prefix = 0; sh.sel_bits = 0; sh.sel_k = k; }
     __syncthreads();
-    select_bucket(sh, kDigitBits);
-    while (sh.sel_cnt > kCandCap && sh.sel_bits < 64) {
+    while (sh.sel_bits < 64) {
         const int bits = sh.sel_bits;
-        const int dbits = (64 - bits) < kDigitBits ? (64 - bits) : kDigitBits;
+        const int dbits = (64 - bits) < kRadixBits ? (64 - bits) : kRadixBits;
         const uint64_t prefix = sh.sel_prefix;
+        const int shift = 64 - bits - dbits;
         for (int i = tid; i < (1 << dbits); i += kThreads) sh.hist[i] = 0;
         __syncthreads();
-        const int shift = 64 - bits - dbits;
         for (int s = tid; s < M; s += kThreads) {
             const double r = res[s];
             if (r == __builtin_inf()) continue;
-            const uint64_t key = dkey(sel_val<kMad>(r, med));
-            if ((key >> (64 - bits)) == prefix) atomicAdd(&sh.hist[(key >> shift) & ((1u << dbits) - 1)], 1u);
+            const double v = sel_val<kMad>(r, med);
+            if ((uint32_t)sel_bin<kMad>(v) != bin) continue;
+            const uint64_t key = dkey(v);
+            if (bits == 0 || (key >> (64 - bits)) == prefix)
+                atomicAdd(&sh.hist[(key >> shift) & ((1u << dbits) - 1)], 1u);
         }
         __syncthreads();
-        select_bucket(sh, dbits);
-    }
-    if (sh.sel_bits >= 64) {  // every bit fixed: the prefix is the key
-        const double v = dkey_inv(sh.sel_prefix);
+        find_bin(sh, sh.hist, 1 << dbits);
+        if (tid == 0) {
+            sh.sel_prefix = (sh.sel_prefix << dbits) | sh.sel_bin;
+            sh.sel_bits += dbits;
+        }
         __syncthreads();
-        return v;
     }
-    // gather the (few) candidates of the bucket and rank them exactly
-    {
-        const int bits = sh.sel_bits;
-        const uint64_t prefix = sh.sel_prefix;
-        for (int s = tid; s < M; s += kThreads) {
-            const double r = res[s];
-            if (r == __builtin_inf()) continue;
-            const uint64_t key = dkey(sel_val<kMad>(r, med));
-            if ((key >> (64 - bits)) == prefix) {
-                const uint32_t slot = atomicAdd(&sh.cand_n, 1u);
-                if (slot < kCandCap) sh.cand[slot] = key;
-            }
-        }
-    }
-    __syncthreads();
-    const uint32_t n = sh.cand_n, kk = sh.sel_k;
-    for (uint32_t i = tid; i < n; i += kThreads) {
-        const uint64_t ki = sh.cand[i];
-        uint32_t less = 0, eq_before = 0;
-        for (uint32_t j = 0; j < n; ++j) {
-            const uint64_t kj = sh.cand[j];
-            less += kj < ki;
-            eq_before += (kj == ki) & (j < i);
-        }
-        if (less + eq_before == kk) sh.sel_value = dkey_inv(ki);
-    }
-    __syncthreads();
-    const double v = sh.sel_value;
+    const double v = dkey_inv(sh.sel_prefix);
     __syncthreads();
     return v;
 }
 
-// (mid-1)-th order statistic given hi = mid-th: hi itself if fewer than mid values are < hi,
-// else the largest value < hi.
+// (k-1)-th order statistic from the k-th (hi): hi itself if at most k-1 values are < hi, else max(<hi)
 template <bool kMad>
-__device__ double block_lower_neighbour(Shared& sh, const double* __restrict__ res, int M, uint32_t mid, double hi,
+__device__ double lower_neighbour_sweep(Shared& sh, const double* __restrict__ res, int M, uint32_t k, double hi,
                                         double med) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t less = 0;
@@ -200,23 +226,123 @@ __device__ double block_lower_neighbour(Shared& sh, const double* __restrict__ r
     double tm = -__builtin_inf();
     for (int w = 0; w < kWaves; ++w) { tl += sh.ired[w][0]; tm = fmax(tm, sh.red[w][0]); }
     __syncthreads();
-    return (tl <= mid - 1) ? hi : tm;
+    return (tl <= k - 1) ? hi : tm;
 }
 
-// computeMedian(v, n) with exact order statistics: odd/even decided by the TOTAL length M
-// (src/algorithm.cpp:845-851); mid == 0 reads vec[mid] (the reference's vec[-1] is UB).
+// computeMedian(v, n) with exact order statistics (odd/even decided by the TOTAL length M,
+// src/algorithm.cpp:845-851; mid == 0 reads vec[mid]).  sh.hist holds the value-bin histogram.
 template <bool kMad>
 __device__ double block_median(Shared& sh, const double* __restrict__ res, int M, uint32_t n, double med) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t mid = n / 2;
-    const double hi = block_select<kMad>(sh, res, M, mid, med);
-    if ((M & 1) || mid == 0) return hi;
-    const double lo = block_lower_neighbour<kMad>(sh, res, M, mid, hi, med);
-    return (lo + hi) / 2.0;
+    const bool want_lo = ((M & 1) == 0) && mid > 0;
+    if (tid == 0) { sh.sel_k = mid; sh.cand_n = 0; }
+    __syncthreads();
+    find_bin(sh, sh.hist, kBins);
+    const uint32_t bin = sh.sel_bin, kk = sh.sel_k, cnt = sh.sel_cnt;
+    double hi, lo = 0.0;
+    if (cnt <= (uint32_t)kCandCap) {
+        double below = -__builtin_inf();
+        for (int s2 = 2 * tid; s2 < M; s2 += 2 * kThreads) {
+            const double2 rr = *reinterpret_cast<const double2*>(res + s2);
+            const double rv[2] = {rr.x, rr.y};
+            for (int j = 0; j < 2; ++j) {
+                if (s2 + j >= M || rv[j] == __builtin_inf()) continue;
+                const double v = sel_val<kMad>(rv[j], med);
+                const uint32_t b = (uint32_t)sel_bin<kMad>(v);
+                if (b == bin) sh.cand[atomicAdd(&sh.cand_n, 1u)] = v;
+                else if (b < bin) below = fmax(below, v);
+            }
+        }
+        below = wave_max(below);
+        if (lane == 0) sh.red[wave][0] = below;
+        __syncthreads();
+        double tb = -__builtin_inf();
+        for (int w = 0; w < kWaves; ++w) tb = fmax(tb, sh.red[w][0]);
+        cand_select(sh, cnt, kk, want_lo);
+        hi = sh.sel_hi;
+        if (want_lo) lo = kk > 0 ? sh.sel_lo : tb;
+        __syncthreads();
+    } else {
+        hi = radix_in_bin<kMad>(sh, res, M, bin, kk, med);
+        if (want_lo) lo = lower_neighbour_sweep<kMad>(sh, res, M, mid, hi, med);
+    }
+    return want_lo ? (lo + hi) / 2.0 : hi;
+}
+
+// bilinearInterpolationDouble (src/algorithm.cpp:896-905) reading a staged window whose top-left
+// image pixel is (ox, oy); cells past the image edge hold 0 and only ever carry a zero weight.
+__device__ __forceinline__ double bilerp_win(const uint8_t* win, int ww, int ox, int oy, double x, double y) {
+    const int32_t x1 = (int32_t)x, y1 = (int32_t)y, x2 = x1 + 1, y2 = y1 + 1;
+    const uint8_t* r1 = win + (y1 - oy) * ww - ox;
+    const uint8_t* r2 = r1 + ww;
+    const double a = (x2 - x) * r1[x1] + (x - x1) * r1[x2];
+    const double b = (x2 - x) * r2[x1] + (x - x1) * r2[x2];
+    return (y2 - y) * a + (y - y1) * b;
+}
+
+__device__ __forceinline__ void stage_window(uint8_t* dst, const uint8_t* img, int W, int H, int ox, int oy, int ww,
+                                             int sub, int lpf) {
+    const int64_t plane = (int64_t)W * H;
+    for (int i = sub; i < ww * ww; i += lpf) {
+        const int ry = i / ww, rx = i - ry * ww;
+        const int64_t lin = (int64_t)(oy + ry) * W + (ox + rx);
+        dst[i] = (lin >= 0 && lin < plane) ? img[lin] : (uint8_t)0;
+    }
+}
+
+// One damped Gauss-Newton step from the reduced sums in sh.tot (src/optimizer.cpp:279-334):
+// lambda = 1e-2 * max diag(H); H_ii += lambda; dx = LDLT(H) \ g; pose <- pose * exp(-dx);
+// status as the reference's single iteration leaves it; err = sqrt(chi2 / n) at the pre-update pose.
+__device__ __attribute__((noinline)) void lm_step(Shared& sh, svo_level_trace& t, uint32_t n, double med, double mad,
+                                                  double sigma) {
+    double g[6], dx[6];
+    int q = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j <= i; ++j) {
+            const double v = sh.tot[q++];
+            sh.A[i * 6 + j] = v;
+            sh.A[j * 6 + i] = v;
+        }
+    for (int i = 0; i < 6; ++i) g[i] = sh.tot[21 + i];
+    const double chi = sh.tot[27];
+    double mx = sh.A[0];
+    for (int i = 1; i < 6; ++i) mx = fmax(mx, sh.A[i * 7]);
+    const double lambda = 1e-2 * mx;
+    for (int i = 0; i < 6; ++i) sh.A[i * 7] += lambda;
+    for (int i = 0; i < 36; ++i) t.H[i] = sh.A[i];
+    ldlt_solve_ws(6, sh.A, g, dx, sh.perm, sh.tmp);
+    double m[6];
+    for (int i = 0; i < 6; ++i) m[i] = -dx[i];
+    sh.pose = se3_compose(sh.pose, se3_exp(m));
+    bool big = false, nan = false;
+    for (int i = 0; i < 6; ++i) { big |= dx[i] > 1e3; nan |= isnan(dx[i]); }
+    int32_t st = kSuccess;
+    if (big) st = kMaxCoffDx;
+    else if (nan) st = kNonInDx;
+    else {
+        double step = 0.0;
+        for (int i = 0; i < 6; ++i) step += dx[i] * dx[i];
+        st = step < 1e-16 ? kSmallStepSize : st;
+        st = fabs(lambda) >= 1e14 ? kLambdaValue : st;
+    }
+    const double e = sqrt(chi / (double)n);
+    t.n_vis = (int32_t)n; t.status = st;
+    t.median = med; t.mad = mad; t.sigma = sigma; t.chi2 = chi; t.lambda = lambda; t.err = e;
+    for (int i = 0; i < 6; ++i) { t.g[i] = g[i]; t.dx[i] = dx[i]; }
+    sh.red[0][28] = e;
+    sh.ired[0][3] = (uint32_t)st;
 }
 
 }  // namespace
 
-__global__ void __launch_bounds__(kThreads) align_pairs_kernel(AlignArgs a) {
+// kStamps: diagnostic build (SVO_PHASE_STAMPS=1) — lane 0 writes s_memtime at each phase boundary to
+// a.stamps[pair][level][8]; no stamp executes in the production instantiation.
+#define SVO_STAMP(i) \
+    if (kStamps && tid == 0) a.stamps[((int64_t)pair * (a.max_level + 1) + level) * 8 + (i)] = __builtin_amdgcn_s_memtime()
+
+template <bool kStamps>
+__global__ void __launch_bounds__(kThreads, 4) align_pairs_kernel(AlignArgs a) {
     __shared__ Shared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pair = blockIdx.x;
@@ -224,6 +350,11 @@ __global__ void __launch_bounds__(kThreads) align_pairs_kernel(AlignArgs a) {
     const int nf = P.n_ref + P.n_kf;
     const int A = a.area, h = a.half, side = 2 * a.half + 1;
     const int M = nf * A;
+    // lane groups: lpf lanes per feature, fpw features per wave
+    const int lpf = A <= 16 ? 16 : (A <= 32 ? 32 : 64);
+    const int fpw = 64 / lpf;
+    const int sub = lane & (lpf - 1), slotw = lane / lpf;
+    const int RW = 2 * h + 5, CW = 2 * h + 3, wbytes = RW * RW + CW * CW;
     const int64_t fbase = (int64_t)pair * a.max_f;
     const double* __restrict__ px = a.px + 2 * fbase;
     const double* __restrict__ bearing = a.bearing + 3 * fbase;
@@ -233,20 +364,18 @@ __global__ void __launch_bounds__(kThreads) align_pairs_kernel(AlignArgs a) {
     double* __restrict__ jimg = a.jimg + 12 * fbase;
     double* __restrict__ cuv = a.cuv + 2 * fbase;
     uint8_t* __restrict__ fvis = a.fvis + fbase;
-    double* __restrict__ res = a.res + fbase * A;
+    double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
     svo_level_trace* traces = a.traces + (int64_t)pair * (a.max_level + 1);
+    uint8_t* wbuf = sh.win[wave] + slotw * wbytes;
 
-    if (tid == 0) {
-        sh.pose = se3_load(P.cur_pose);
-        sh.done = 0;
-    }
+    if (tid == 0) sh.pose = se3_load(P.cur_pose);
     for (int l = tid; l <= a.max_level; l += kThreads) {
         svo_level_trace t = {};
         t.level = l;
         t.status = kFailed;
         traces[l] = t;
     }
-    if (P.n_ref == 0 || M < 6) {  // align(): no ref features -> return 0 (:27-28); optimizeLM: M < 6
+    if (P.n_ref == 0 || M < 6) {  // align(): no ref features -> 0 (:27-28); optimizeLM: M < 6 (:173-174)
         if (tid == 0) {
             se3_store(sh.pose, a.pose_out + 7 * pair);
             a.err_out[pair] = P.n_ref == 0 ? 0.0 : -1.0;
@@ -263,9 +392,8 @@ __global__ void __launch_bounds__(kThreads) align_pairs_kernel(AlignArgs a) {
         for (int f = tid; f < nf; f += kThreads) {
             if (!has_point[f]) continue;
             const bool is_ref = f < P.n_ref;
-            const V3 C = is_ref ? Cr : Ck;
             const V3 Pw{point[3 * f], point[3 * f + 1], point[3 * f + 2]};
-            const double depth = v3norm(v3sub(Pw, C));
+            const double depth = v3norm(v3sub(Pw, is_ref ? Cr : Ck));
             const V3 pc = v3scl(V3{bearing[3 * f], bearing[3 * f + 1], bearing[3 * f + 2]}, depth);
             const V3 pw = se3_act(is_ref ? Tri : Tki, pc);
             xw[3 * f] = pw.x; xw[3 * f + 1] = pw.y; xw[3 * f + 2] = pw.z;
@@ -277,6 +405,7 @@ __global__ void __launch_bounds__(kThreads) align_pairs_kernel(AlignArgs a) {
     int32_t status = kFailed;
     for (int level = a.max_level; level >= a.min_level; --level) {
         const int32_t W = a.geom.w[level], H = a.geom.h[level];
+        SVO_STAMP(0);
         const int64_t loff = a.geom.off[level];
         const uint8_t* __restrict__ ref_img = P.ref_pyr + loff;
         const uint8_t* __restrict__ kf_img = P.kf_pyr + loff;
@@ -284,160 +413,177 @@ __global__ void __launch_bounds__(kThreads) align_pairs_kernel(AlignArgs a) {
         const double dom = (double)(1 << level), scale = 1.0 / dom;
         const double lfx = a.fx / dom, lfy = a.fy / dom;
         const int border = h + 2;
-        const SE3 pose = sh.pose;
 
-        // ---- P1: per-feature visibility, projection and image Jacobian
-        uint32_t cnt[4] = {0, 0, 0, 0};
-        for (int f = tid; f < nf; f += kThreads) {
-            uint8_t vis = 0;
-            if (has_point[f]) {
-                const double u = px[2 * f] * scale, v = px[2 * f + 1] * scale;
-                const int ui = (int)floor(u), vi = (int)floor(v);
-                if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
-                    vis = 1;
-                    const V3 pw{xw[3 * f], xw[3 * f + 1], xw[3 * f + 2]};
-                    double ja[6], jb[6];
-                    image_jac(pw, lfx, lfy, ja, jb);
-                    for (int j = 0; j < 6; ++j) { jimg[12 * f + j] = ja[j]; jimg[12 * f + 6 + j] = jb[j]; }
-                    const V3 cp = se3_act(pose, pw);
-                    const double cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
-                    const double cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
-                    const int cui = (int)floor(cu), cvi = (int)floor(cv);
-                    if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H)) {
-                        vis = 3;
-                        cuv[2 * f] = cu;
-                        cuv[2 * f + 1] = cv;
+        // ---- P1: per-feature visibility, projection into cur, image Jacobian
+        {
+            const SE3 pose = sh.pose;
+            uint32_t nrv = 0, ncv = 0;
+            for (int f = tid; f < nf; f += kThreads) {
+                uint8_t vis = 0;
+                if (has_point[f]) {
+                    const double u = px[2 * f] * scale, v = px[2 * f + 1] * scale;
+                    const int ui = (int)floor(u), vi = (int)floor(v);
+                    if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
+                        vis = 1;
+                        const V3 pw{xw[3 * f], xw[3 * f + 1], xw[3 * f + 2]};
+                        const V3 cp = se3_act(pose, pw);
+                        const double cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
+                        const double cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
+                        const int cui = (int)floor(cu), cvi = (int)floor(cv);
+                        if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H)) {
+                            vis = 3;
+                            cuv[2 * f] = cu;
+                            cuv[2 * f + 1] = cv;
+                            double ja[6], jb[6];
+                            image_jac(pw, lfx, lfy, ja, jb);
+                            for (int j = 0; j < 6; ++j) { jimg[12 * f + j] = ja[j]; jimg[12 * f + 6 + j] = jb[j]; }
+                        }
                     }
                 }
+                fvis[f] = vis;
+                nrv += vis & 1;
+                ncv += vis >> 1;
             }
-            fvis[f] = vis;
-            cnt[0] += vis & 1;
-            cnt[1] += vis >> 1;
+            block_sum_u2(sh, nrv, ncv);
+            if (tid == 0) {
+                traces[level].n_ref_vis = (int32_t)nrv;
+                sh.ired[0][2] = ncv;
+            }
         }
-        block_sum_u4(sh, cnt);
-        const uint32_t n_ref_vis = cnt[0];
-        const uint32_t n = cnt[1] * (uint32_t)A;
-
-        // ---- P2: residuals (+inf for invisible slots) and first radix digit of the median
         for (int i = tid; i < kBins; i += kThreads) sh.hist[i] = 0;
         __syncthreads();
-        for (int s = tid; s < M; s += kThreads) {
-            const int f = s / A, k = s - f * A;
-            double r = __builtin_inf();
-            if (fvis[f] == 3) {
-                const int ky = k / side - h, kx = k - (k / side) * side - h;
-                const uint8_t* rimg = f < P.n_ref ? ref_img : kf_img;
-                const double T = bilinear_d(rimg, W, px[2 * f] * scale + kx, px[2 * f + 1] * scale + ky);
-                const double I = bilinear_d(cur_img, W, cuv[2 * f] + kx, cuv[2 * f + 1] + ky);
-                r = I - T;
-                atomicAdd(&sh.hist[dkey(r) >> (64 - kDigitBits)], 1u);
-            }
-            res[s] = r;
-        }
-        __syncthreads();
+        SVO_STAMP(1);
+        const uint32_t n = sh.ired[0][2] * (uint32_t)A;
 
-        // ---- P3/P4: robust scale  (Optimizer::tukeyWeighting -> algorithm::computeSigma)
+        // ---- S1: residuals through LDS-staged windows; value-bin histogram of r
+        for (int g = wave; g * fpw < nf; g += kWaves) {
+            const int f = g * fpw + slotw;
+            const bool fv = f < nf && fvis[f] == 3;
+            double ur = 0, vr = 0, cu = 0, cv = 0;
+            int rox = 0, roy = 0, cox = 0, coy = 0;
+            if (fv) {
+                ur = px[2 * f] * scale; vr = px[2 * f + 1] * scale;
+                cu = cuv[2 * f]; cv = cuv[2 * f + 1];
+                rox = (int)floor(ur) - h - 1; roy = (int)floor(vr) - h - 1;
+                cox = (int)floor(cu) - h; coy = (int)floor(cv) - h;
+                stage_window(wbuf, f < P.n_ref ? ref_img : kf_img, W, H, rox, roy, RW, sub, lpf);
+                stage_window(wbuf + RW * RW, cur_img, W, H, cox, coy, CW, sub, lpf);
+            }
+            wave_lds_sync();
+            if (f < nf) {
+                for (int k = sub; k < A; k += lpf) {
+                    double r = __builtin_inf();
+                    if (fv) {
+                        const int ky = k / side - h, kx = k - (k / side) * side - h;
+                        const double T = bilerp_win(wbuf, RW, rox, roy, ur + kx, vr + ky);
+                        const double I = bilerp_win(wbuf + RW * RW, CW, cox, coy, cu + kx, cv + ky);
+                        r = I - T;
+                        atomicAdd(&sh.hist[sel_bin<false>(r)], 1u);
+                    }
+                    res[f * A + k] = r;
+                }
+            }
+            wave_lds_sync();
+        }
+        if (tid == 0 && (M & 1)) res[M] = __builtin_inf();  // pad for the double2 sweeps
+        __syncthreads();
+        SVO_STAMP(2);
+
+        // ---- S2-S4: robust scale  (Optimizer::tukeyWeighting -> algorithm::computeSigma)
         double med, mad;
         if (n == 0) {
             med = 1.7976931348623157e308;  // every slot is DBL_MAX in the reference
             mad = 0.0;
         } else {
             med = block_median<false>(sh, res, M, n, 0.0);
+            SVO_STAMP(3);
             for (int i = tid; i < kBins; i += kThreads) sh.hist[i] = 0;
             __syncthreads();
-            for (int s = tid; s < M; s += kThreads) {
-                const double r = res[s];
-                if (r == __builtin_inf()) continue;
-                atomicAdd(&sh.hist[dkey(fabs(r - med)) >> (64 - kDigitBits)], 1u);
+            for (int s2 = 2 * tid; s2 < M; s2 += 2 * kThreads) {
+                const double2 rr = *reinterpret_cast<const double2*>(res + s2);
+                if (rr.x != __builtin_inf()) atomicAdd(&sh.hist[sel_bin<true>(fabs(rr.x - med))], 1u);
+                if (s2 + 1 < M && rr.y != __builtin_inf()) atomicAdd(&sh.hist[sel_bin<true>(fabs(rr.y - med))], 1u);
             }
             __syncthreads();
             mad = block_median<true>(sh, res, M, n, med);
         }
+        SVO_STAMP(4);
         double sigma = 1.482602218505602 * mad;
         if (sigma <= 2.220446049250313e-16) sigma = 2.220446049250313e-16;
         const double c = 4.6851 * sigma, c2 = c * c;
 
-        // ---- P5: Tukey weights, chi2, normal equations (lower triangle, as the LDLT reads it)
-        double acc[28];
-        for (int i = 0; i < 28; ++i) acc[i] = 0.0;
-        for (int s = tid; s < M; s += kThreads) {
-            const double r = res[s];
-            if (r == __builtin_inf()) continue;
-            double w = 0.0;
-            if (fabs(r) <= c) {
-                const double t = 1.0 - (r * r) / c2;
-                w = t * t;
+        // ---- S5: Tukey weights, chi2, factorised normal equations (lower triangle)
+        double chi_acc = 0.0;
+        if (lane < 28) sh.accw[wave][lane] = 0.0;
+        wave_lds_sync();
+        for (int g = wave; g * fpw < nf; g += kWaves) {
+            const int f = g * fpw + slotw;
+            const bool fv = f < nf && fvis[f] == 3;
+            double ur = 0, vr = 0;
+            int rox = 0, roy = 0;
+            if (fv) {
+                ur = px[2 * f] * scale; vr = px[2 * f + 1] * scale;
+                rox = (int)floor(ur) - h - 1; roy = (int)floor(vr) - h - 1;
+                stage_window(wbuf, f < P.n_ref ? ref_img : kf_img, W, H, rox, roy, RW, sub, lpf);
             }
-            acc[27] += r * r * w;
-            if (w == 0.0) continue;
-            const int f = s / A, k = s - f * A;
-            const int ky = k / side - h, kx = k - (k / side) * side - h;
-            const uint8_t* rimg = f < P.n_ref ? ref_img : kf_img;
-            const double row = px[2 * f + 1] * scale + ky, col = px[2 * f] * scale + kx;
-            const double dx = 0.5 * (bilinear_d(rimg, W, col + 1, row) - bilinear_d(rimg, W, col - 1, row));
-            const double dy = 0.5 * (bilinear_d(rimg, W, col, row + 1) - bilinear_d(rimg, W, col, row - 1));
-            double J[6];
-            for (int j = 0; j < 6; ++j) J[j] = dx * jimg[12 * f + j] + dy * jimg[12 * f + 6 + j];
-            int q = 0;
-            for (int i = 0; i < 6; ++i) {
-                const double jw = J[i] * w;
-                for (int j = 0; j <= i; ++j) acc[q++] += jw * J[j];
-                acc[21 + i] += jw * r;
+            wave_lds_sync();
+            double sxx = 0, sxy = 0, syy = 0, sxr = 0, syr = 0;
+            if (fv) {
+                for (int k = sub; k < A; k += lpf) {
+                    const double r = res[f * A + k];
+                    double w = 0.0;
+                    if (fabs(r) <= c) {
+                        const double t = 1.0 - (r * r) / c2;
+                        w = t * t;
+                    }
+                    chi_acc += r * r * w;
+                    if (w == 0.0) continue;
+                    const int ky = k / side - h, kx = k - (k / side) * side - h;
+                    const double row = vr + ky, col = ur + kx;
+                    const double dx = 0.5 * (bilerp_win(wbuf, RW, rox, roy, col + 1, row) -
+                                             bilerp_win(wbuf, RW, rox, roy, col - 1, row));
+                    const double dy = 0.5 * (bilerp_win(wbuf, RW, rox, roy, col, row + 1) -
+                                             bilerp_win(wbuf, RW, rox, roy, col, row - 1));
+                    const double wdx = w * dx, wdy = w * dy;
+                    sxx += wdx * dx; sxy += wdx * dy; syy += wdy * dy; sxr += wdx * r; syr += wdy * r;
+                }
+            }
+            for (int o = lpf >> 1; o > 0; o >>= 1) {
+                sxx += __shfl_down(sxx, o, lpf); sxy += __shfl_down(sxy, o, lpf); syy += __shfl_down(syy, o, lpf);
+                sxr += __shfl_down(sxr, o, lpf); syr += __shfl_down(syr, o, lpf);
+            }
+            for (int j = 0; j < fpw; ++j) {  // the wave's features one after another: fixed order
+                if (fv && sub == 0 && slotw == j) {
+                    double ja[6], jb[6];
+                    for (int t = 0; t < 6; ++t) { ja[t] = jimg[12 * f + t]; jb[t] = jimg[12 * f + 6 + t]; }
+                    double* acc = sh.accw[wave];
+                    int q = 0;
+                    for (int i = 0; i < 6; ++i) {
+                        for (int t = 0; t <= i; ++t)
+                            acc[q++] += ja[i] * ja[t] * sxx + (ja[i] * jb[t] + jb[i] * ja[t]) * sxy + jb[i] * jb[t] * syy;
+                        acc[21 + i] += ja[i] * sxr + jb[i] * syr;
+                    }
+                }
+                wave_lds_sync();
             }
         }
-        for (int i = 0; i < 28; ++i) {
-            const double v = wave_sum(acc[i]);
-            if (lane == 0) sh.red[wave][i] = v;
-        }
+        chi_acc = wave_sum(chi_acc);
+        if (lane == 0) sh.accw[wave][27] = chi_acc;
         __syncthreads();
+        SVO_STAMP(5);
 
-        // ---- P6: damped step, solve, update (one lane)
-        if (tid == 0) {
-            double tot[28];
-            for (int i = 0; i < 28; ++i) {
-                double s = 0.0;
-                for (int w = 0; w < kWaves; ++w) s += sh.red[w][i];
-                tot[i] = s;
-            }
-            double Hm[36], g[6], dx[6];
-            int q = 0;
-            for (int i = 0; i < 6; ++i)
-                for (int j = 0; j <= i; ++j) { Hm[i * 6 + j] = tot[q]; Hm[j * 6 + i] = tot[q]; ++q; }
-            for (int i = 0; i < 6; ++i) g[i] = tot[21 + i];
-            const double chi = tot[27];
-            double mx = Hm[0];
-            for (int i = 1; i < 6; ++i) mx = fmax(mx, Hm[i * 6 + i]);
-            const double lambda = 1e-2 * mx;
-            for (int i = 0; i < 6; ++i) Hm[i * 6 + i] += lambda;
-            ldlt_solve(6, Hm, g, dx);
-            double m[6];
-            for (int i = 0; i < 6; ++i) m[i] = -dx[i];
-            SE3 np = se3_compose(sh.pose, se3_exp(m));
-            sh.pose = np;
-            bool big = false, nan = false;
-            for (int i = 0; i < 6; ++i) { big |= dx[i] > 1e3; nan |= isnan(dx[i]); }
-            int32_t st = kSuccess;
-            if (big) st = kMaxCoffDx;
-            else if (nan) st = kNonInDx;
-            else {
-                double step = 0.0;
-                for (int i = 0; i < 6; ++i) step += dx[i] * dx[i];
-                st = step < 1e-16 ? kSmallStepSize : st;
-                st = fabs(lambda) >= 1e14 ? kLambdaValue : st;
-            }
-            const double e = sqrt(chi / (double)n);
-            svo_level_trace t;
-            t.level = level; t.n_ref_vis = (int32_t)n_ref_vis; t.n_vis = (int32_t)n; t.status = st;
-            t.median = med; t.mad = mad; t.sigma = sigma; t.chi2 = chi; t.lambda = lambda; t.err = e;
-            for (int i = 0; i < 36; ++i) t.H[i] = Hm[i];
-            for (int i = 0; i < 6; ++i) { t.g[i] = g[i]; t.dx[i] = dx[i]; }
-            traces[level] = t;
-            sh.red[0][0] = e;
-            sh.ired[0][0] = (uint32_t)st;
+        // ---- P6: damped step, solve, update (one lane; LDS workspace)
+        if (tid < 28) {  // wave partials in a fixed order
+            double s = 0.0;
+            for (int w = 0; w < kWaves; ++w) s += sh.accw[w][tid];
+            sh.tot[tid] = s;
         }
         __syncthreads();
-        err = sh.red[0][0];
-        status = (int32_t)sh.ired[0][0];
+        if (tid == 0) lm_step(sh, traces[level], n, med, mad, sigma);
+        __syncthreads();
+        SVO_STAMP(6);
+        err = sh.red[0][28];
+        status = (int32_t)sh.ired[0][3];
         __syncthreads();
     }
     if (tid == 0) {
@@ -448,7 +594,17 @@ __global__ void __launch_bounds__(kThreads) align_pairs_kernel(AlignArgs a) {
 }
 
 void launch_align(const AlignArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(align_pairs_kernel, dim3(a.n_pairs), dim3(kThreads), 0, s, a);
+    if (a.stamps)
+        hipLaunchKernelGGL(align_pairs_kernel<true>, dim3(a.n_pairs), dim3(kThreads), 0, s, a);
+    else
+        hipLaunchKernelGGL(align_pairs_kernel<false>, dim3(a.n_pairs), dim3(kThreads), 0, s, a);
 }
+
+int align_window_bytes(int half) {
+    const int A = (2 * half + 1) * (2 * half + 1);
+    const int fpw = A <= 16 ? 4 : (A <= 32 ? 2 : 1);
+    return fpw * ((2 * half + 5) * (2 * half + 5) + (2 * half + 3) * (2 * half + 3));
+}
+int align_window_capacity() { return kWinBytes; }
 
 }  // namespace svo

@@ -3,6 +3,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -67,6 +68,7 @@ struct svo_align_batch {
     svo_camera cam;
     svo_align_params params;
     int32_t n_pairs, max_f, half, area;
+    int64_t res_stride;
     svo::LevelGeom geom;
     std::vector<svo::PairDesc> h_pairs;
     std::vector<uint8_t> pair_set;
@@ -75,6 +77,7 @@ struct svo_align_batch {
     uint8_t *d_has_point, *d_fvis;
     int32_t* d_status;
     svo_level_trace* d_traces;
+    unsigned long long* d_stamps;  // SVO_PHASE_STAMPS=1 diagnostics
     bool ran;
 };
 
@@ -233,7 +236,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_jimg,
-                    b->d_cuv, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
+                    b->d_cuv, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces, b->d_stamps};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -243,7 +246,8 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     if (!c || !cam || !prm || !out) return fail(SVO_ERR_ARG, "null argument");
     *out = nullptr;
     if (n_pairs <= 0 || max_features <= 0) return fail(SVO_ERR_ARG, "n_pairs and max_features must be > 0");
-    if (prm->patch_size < 1 || prm->patch_size > 31) return fail(SVO_ERR_ARG, "patch_size %d unsupported", prm->patch_size);
+    if (prm->patch_size < 1 || svo::align_window_bytes(prm->patch_size / 2) > svo::align_window_capacity())
+        return fail(SVO_ERR_ARG, "patch_size %d unsupported (<= 19)", prm->patch_size);
     if (prm->min_level < 0 || prm->max_level < prm->min_level || prm->max_level >= svo::kMaxLevels)
         return fail(SVO_ERR_ARG, "bad level range [%d,%d]", prm->min_level, prm->max_level);
     if (prm->median_mode != 0) return fail(SVO_ERR_ARG, "median_mode %d not implemented (0 = exact)", prm->median_mode);
@@ -269,11 +273,14 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_jimg, F * 12 * sizeof(double));
     ALLOC(b->d_cuv, F * 2 * sizeof(double));
     ALLOC(b->d_fvis, F);
-    ALLOC(b->d_res, F * area * sizeof(double));
+    b->res_stride = ((int64_t)max_features * area + 2 + 63) / 64 * 64;
+    ALLOC(b->d_res, (size_t)n_pairs * b->res_stride * sizeof(double));
     ALLOC(b->d_pose_out, (size_t)n_pairs * 7 * sizeof(double));
     ALLOC(b->d_err, (size_t)n_pairs * sizeof(double));
     ALLOC(b->d_status, (size_t)n_pairs * sizeof(int32_t));
     ALLOC(b->d_traces, (size_t)n_pairs * (prm->max_level + 1) * sizeof(svo_level_trace));
+    { const char* env = getenv("SVO_PHASE_STAMPS");
+      if (env && env[0] == '1') ALLOC(b->d_stamps, (size_t)n_pairs * (prm->max_level + 1) * 8 * sizeof(unsigned long long)); }
 #undef ALLOC
     if (e != hipSuccess) {
         free_batch(b);
@@ -360,8 +367,9 @@ int svo_align_batch_run(svo_align_batch* b) {
     svo::AlignArgs a;
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
-    a.xw = b->d_xw; a.jimg = b->d_jimg; a.cuv = b->d_cuv; a.fvis = b->d_fvis; a.res = b->d_res;
+    a.xw = b->d_xw; a.jimg = b->d_jimg; a.cuv = b->d_cuv; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
+    a.stamps = b->d_stamps;
     a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
     a.min_level = b->params.min_level; a.max_level = b->params.max_level;
     a.fx = b->cam.fx; a.fy = b->cam.fy; a.cx = b->cam.cx; a.cy = b->cam.cy;
@@ -456,3 +464,14 @@ int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, con
 }
 
 }  // extern "C"
+
+extern "C" int svo_align_batch_phase_stamps(svo_align_batch* b, uint64_t* out) {
+    if (!b || !out) return fail(SVO_ERR_ARG, "null argument");
+    if (!b->d_stamps) return fail(SVO_ERR_STATE, "batch created without SVO_PHASE_STAMPS=1");
+    if (!b->ran) return fail(SVO_ERR_STATE, "batch has not been run");
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    const size_t cnt = (size_t)b->n_pairs * (b->params.max_level + 1) * 8;
+    SVO_HIP(hipMemcpyAsync(out, b->d_stamps, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, b->ctx->stream));
+    SVO_HIP(hipStreamSynchronize(b->ctx->stream));
+    return SVO_OK;
+}

@@ -36,17 +36,21 @@ struct AlignArgs {
     double* jimg;             // scratch [n_pairs*max_f][12]  image Jacobian at the current level
     double* cuv;              // scratch [n_pairs*max_f][2]   projection into cur at the current level
     uint8_t* fvis;            // scratch [n_pairs*max_f]      bit0 ref visible, bit1 cur visible
-    double* res;              // scratch [n_pairs*max_f*area] residual per pixel slot (+inf = invisible)
+    double* res;              // scratch [n_pairs][res_stride] residual per pixel slot (+inf = invisible)
+    int64_t res_stride;       // >= max_f*area + 1, even (16-B aligned rows for the double2 sweeps)
     double* pose_out;         // [n_pairs][7]
     double* err_out;          // [n_pairs]
     int32_t* status_out;      // [n_pairs]
     svo_level_trace* traces;  // [n_pairs][max_level+1]
+    unsigned long long* stamps;  // diagnostics: [n_pairs][max_level+1][8] s_memtime per phase, or null
     int32_t n_pairs, max_f, half, area, min_level, max_level;
     double fx, fy, cx, cy;
     LevelGeom geom;
 };
 
 void launch_align(const AlignArgs& a, hipStream_t s);
+int align_window_bytes(int half);  // LDS staging bytes one wave needs for this half patch size
+int align_window_capacity();       // LDS staging bytes available per wave
 void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t count, hipStream_t s);
 
 struct FeatureAlignArgs {

@@ -108,12 +108,10 @@ SVO_HD void se3_store(const SE3& T, double* p) {
     p[0] = T.q.x; p[1] = T.q.y; p[2] = T.q.z; p[3] = T.q.w; p[4] = T.t.x; p[5] = T.t.y; p[6] = T.t.z;
 }
 
-// Eigen LDLT<.., Lower> factor + solve, n <= 6, row-major input (lower triangle read).
-SVO_HD void ldlt_solve(int n, const double* Hin, const double* b, double* x) {
-    double A[36];
-    for (int i = 0; i < n * n; ++i) A[i] = Hin[i];
-    int perm[6];
-    double tmp[6];
+// Eigen LDLT<.., Lower> factor + solve, n <= 6, row-major A (lower triangle read), factored in place.
+// A / perm / tmp are caller workspace (registers, or LDS so that no thread keeps 36 doubles live).
+template <typename Real, typename Int>
+SVO_HD void ldlt_solve_ws(int n, Real* A, const double* b, double* x, Int* perm, Real* tmp) {
     for (int k = 0; k < n; ++k) {
         int piv = k;
         double best = fabs(A[k * n + k]);
@@ -166,6 +164,12 @@ SVO_HD void ldlt_solve(int n, const double* Hin, const double* b, double* x) {
         x[i] = s;
     }
     for (int k = n - 1; k >= 0; --k) { double t = x[k]; x[k] = x[perm[k]]; x[perm[k]] = t; }
+}
+SVO_HD void ldlt_solve(int n, const double* Hin, const double* b, double* x) {
+    double A[36], tmp[6];
+    int perm[6];
+    for (int i = 0; i < n * n; ++i) A[i] = Hin[i];
+    ldlt_solve_ws(n, A, b, x, perm, tmp);
 }
 
 // algorithm::bilinearInterpolationDouble — row-major u8 image with row pitch `w`
