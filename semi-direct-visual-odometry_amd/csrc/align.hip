@@ -2,22 +2,23 @@
 //
 // One 512-thread workgroup owns one frame pair for the whole coarse-to-fine call.  Pairs are
 // independent: no workgroup talks to another, a batch is one launch, and with
-// <= 128 VGPRs and ~62 KB of LDS two pairs share a CU.  Per level:
+// <= 128 VGPRs and ~70 KB of LDS two pairs share a CU.  Per level:
 //   P1  thread / feature : ref visibility (border rule :140-149), projection pose*X_w into cur (:320-340),
 //                          image Jacobian at the WORLD point (:163, :194-248) -> per-feature scratch
-//   S1  lane group / feature (32 lanes for the 25 px of patch 5, 64 for patch 7): the feature's ref
-//                          window ((2h+5)^2 px) and cur window ((2h+3)^2 px) are staged in LDS with a
-//                          few byte loads, then every lane samples its pixel: r = I_cur - T_ref (:359);
-//                          r goes to a per-pair scratch row (+inf = invisible slot), its value bin to an
-//                          LDS histogram (4096 bins of 1/8 grey level)
+//   S1  lane group / feature (32 lanes for the 25 px of patch 5, 64 for patch 7), kUnroll feature
+//                          groups per wave iteration so their loads overlap: the feature's ref window
+//                          ((2h+5)^2 px) and cur window ((2h+3)^2 px) are staged in LDS with a few byte
+//                          loads, then every lane samples its pixel: r = I_cur - T_ref (:359); r goes to a
+//                          per-pair scratch row (+inf = invisible slot), its value bin to an LDS histogram
 //   S2  exact median (src/algorithm.cpp:834-853): the histogram names the bin of rank n/2; one sweep
-//                          gathers that bin's values (plus the max below it) into LDS; exact rank there.
+//                          gathers that bin's values (plus the max below it) into LDS; exact rank there
 //   S3/S4  the same for |r - median| -> MAD -> sigma = 1.482602218505602 * MAD (:855-872)
 //   S5  lane group / feature : Tukey weight (src/optimizer.cpp:485-514), chi2, dx/dy re-sampled from the
-//                          staged ref window; per feature the 5 sums S_xx S_xy S_yy S_xr S_yr (shuffles
-//                          inside the lane group) expand with the 2x6 image Jacobian into the lower
-//                          triangle of J^T W J and J^T W r (factorised J row = dx*Jimg0 + dy*Jimg1);
-//                          wave shuffles + fixed-order LDS tree -> deterministic, no atomics
+//                          staged ref window, per-feature sums S_xx S_xy S_yy S_xr S_yr (shuffles in the
+//                          lane group) -> per-feature scratch
+//   P5b thread / feature : expand the 5 sums with the 2x6 image Jacobian into the lower triangle of
+//                          J^T W J and J^T W r (factorised J row = dx*Jimg0 + dy*Jimg1); wave shuffles +
+//                          fixed-order LDS tree -> deterministic, no atomics
 //   P6  one lane          : Nielsen damping, Eigen-LDLT (LDS workspace), pose <- pose * exp(-dx),
 //                          status, RMSE (src/optimizer.cpp:279-366, src/image_alignment.cpp:379)
 // Exact order statistics: values are binned by a monotone map, so the bin of rank k and its
@@ -33,10 +34,12 @@ namespace {
 constexpr int kThreads = 512;
 constexpr int kWaves = kThreads / 64;
 constexpr int kBins = 4096;
-constexpr double kBinScale = 8.0;  // bins per grey level
+constexpr double kBinScale = 32.0;   // bins per grey level
+constexpr double kBinOffset = 64.0;  // signed map covers [-64, 64); outliers clamp to the end bins
 constexpr int kCandCap = 4096;
-constexpr int kRankCap = 1024;     // <= this many candidates: rank counting, else bitonic sort
-constexpr int kWinBytes = 1024;    // per-wave staging buffer
+constexpr int kRankCap = 256;        // <= this many candidates: rank counting, else bitonic sort
+constexpr int kWinBytes = 2048;      // per-wave staging buffer
+constexpr int kUnroll = 4;           // feature groups in flight per wave iteration
 constexpr int kRadixBits = 11;
 
 struct Shared {
@@ -44,7 +47,8 @@ struct Shared {
     double cand[kCandCap];
     uint8_t win[kWaves][kWinBytes];
     double red[kWaves][30];
-    double accw[kWaves][28];  // per-wave J^T W J (21, lower) | J^T W r (6) | chi2, fixed accumulation order
+    double accw[kWaves][28];  // per-wave J^T W J (21, lower) | J^T W r (6) | chi2
+    double part[kThreads / 32][28];  // P5b partial sums per (feature chunk, term)
     double tot[28];
     uint32_t ired[kWaves][4];
     uint32_t scan[kThreads];
@@ -69,11 +73,14 @@ __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
     return v;
 }
-__device__ __forceinline__ void wave_lds_sync() {  // make this wave's LDS writes visible to its own lanes
+__device__ __forceinline__ void wave_lds_sync() {  // this wave's LDS writes -> visible to its own lanes
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// x / d for small x via a 32-bit magic multiplier (exact for x * d < 2^32)
+__device__ __forceinline__ uint32_t magic_of(uint32_t d) { return (uint32_t)((0x100000000ull + d - 1) / d); }
+__device__ __forceinline__ uint32_t udiv(uint32_t x, uint32_t m) { return __umulhi(x, m); }
 
 // block-wide sums of 2 counters, valid in every thread
 __device__ void block_sum_u2(Shared& sh, uint32_t& a, uint32_t& b) {
@@ -92,11 +99,31 @@ template <bool kMad>
 __device__ __forceinline__ double sel_val(double r, double med) { return kMad ? fabs(r - med) : r; }
 template <bool kMad>
 __device__ __forceinline__ int sel_bin(double v) {
-    const double t = kMad ? v * kBinScale : (v + 256.0) * kBinScale;
+    const double t = kMad ? v * kBinScale : (v + kBinOffset) * kBinScale;
     return t < 0.0 ? 0 : (t >= (double)(kBins - 1) ? kBins - 1 : (int)t);
 }
 
-// bin holding rank sh.sel_k of sh.hist -> sh.sel_bin, sh.sel_k (rank inside the bin), sh.sel_cnt
+// Sweep the residual row with 4 x 16-B loads in flight per lane; fn(value, slot-valid) for each slot.
+// res[M] is +inf when M is odd, so pairs never read past the row.
+template <typename Fn>
+__device__ __forceinline__ void sweep_res(const double* __restrict__ res, int M, Fn fn) {
+    const int tid = threadIdx.x;
+    for (int base = 2 * tid; base < M; base += 8 * kThreads) {
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int s2 = base + u * 2 * kThreads;
+            v[u] = s2 < M ? *reinterpret_cast<const double2*>(res + s2) : make_double2(__builtin_inf(), __builtin_inf());
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (v[u].x != __builtin_inf()) fn(v[u].x);
+            if (v[u].y != __builtin_inf()) fn(v[u].y);
+        }
+    }
+}
+
+// bin holding rank sh.sel_k of hist -> sh.sel_bin, sh.sel_k (rank inside the bin), sh.sel_cnt
 __device__ void find_bin(Shared& sh, const uint32_t* hist, int bins) {
     const int tid = threadIdx.x;
     const uint32_t k = sh.sel_k;
@@ -106,15 +133,19 @@ __device__ void find_bin(Shared& sh, const uint32_t* hist, int bins) {
         const int b = tid * per + i;
         if (b < bins) local += hist[b];
     }
-    sh.scan[tid] = local;
-    __syncthreads();
-    for (int o = 1; o < kThreads; o <<= 1) {
-        const uint32_t add = tid >= o ? sh.scan[tid - o] : 0;
-        __syncthreads();
-        sh.scan[tid] += add;
-        __syncthreads();
+    // block exclusive scan of the per-thread counts: wave scan + wave totals
+    const int lane = tid & 63, wave = tid >> 6;
+    uint32_t incl = local;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
     }
-    const uint32_t incl = sh.scan[tid], excl = incl - local;
+    if (lane == 63) sh.scan[wave] = incl;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; ++w) off += sh.scan[w];
+    incl += off;
+    const uint32_t excl = incl - local;
     if (k >= excl && k < incl) {
         uint32_t run = excl;
         for (int i = 0; i < per; ++i) {
@@ -183,15 +214,13 @@ __device__ double radix_in_bin(Shared& sh, const double* __restrict__ res, int M
         const int shift = 64 - bits - dbits;
         for (int i = tid; i < (1 << dbits); i += kThreads) sh.hist[i] = 0;
         __syncthreads();
-        for (int s = tid; s < M; s += kThreads) {
-            const double r = res[s];
-            if (r == __builtin_inf()) continue;
+        sweep_res(res, M, [&](double r) {
             const double v = sel_val<kMad>(r, med);
-            if ((uint32_t)sel_bin<kMad>(v) != bin) continue;
+            if ((uint32_t)sel_bin<kMad>(v) != bin) return;
             const uint64_t key = dkey(v);
             if (bits == 0 || (key >> (64 - bits)) == prefix)
                 atomicAdd(&sh.hist[(key >> shift) & ((1u << dbits) - 1)], 1u);
-        }
+        });
         __syncthreads();
         find_bin(sh, sh.hist, 1 << dbits);
         if (tid == 0) {
@@ -212,12 +241,10 @@ __device__ double lower_neighbour_sweep(Shared& sh, const double* __restrict__ r
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t less = 0;
     double mx = -__builtin_inf();
-    for (int s = tid; s < M; s += kThreads) {
-        const double r = res[s];
-        if (r == __builtin_inf()) continue;
+    sweep_res(res, M, [&](double r) {
         const double v = sel_val<kMad>(r, med);
         if (v < hi) { ++less; mx = fmax(mx, v); }
-    }
+    });
     less = wave_sum_u(less);
     mx = wave_max(mx);
     if (lane == 0) { sh.ired[wave][0] = less; sh.red[wave][0] = mx; }
@@ -243,17 +270,12 @@ __device__ double block_median(Shared& sh, const double* __restrict__ res, int M
     double hi, lo = 0.0;
     if (cnt <= (uint32_t)kCandCap) {
         double below = -__builtin_inf();
-        for (int s2 = 2 * tid; s2 < M; s2 += 2 * kThreads) {
-            const double2 rr = *reinterpret_cast<const double2*>(res + s2);
-            const double rv[2] = {rr.x, rr.y};
-            for (int j = 0; j < 2; ++j) {
-                if (s2 + j >= M || rv[j] == __builtin_inf()) continue;
-                const double v = sel_val<kMad>(rv[j], med);
-                const uint32_t b = (uint32_t)sel_bin<kMad>(v);
-                if (b == bin) sh.cand[atomicAdd(&sh.cand_n, 1u)] = v;
-                else if (b < bin) below = fmax(below, v);
-            }
-        }
+        sweep_res(res, M, [&](double r) {
+            const double v = sel_val<kMad>(r, med);
+            const uint32_t b = (uint32_t)sel_bin<kMad>(v);
+            if (b == bin) sh.cand[atomicAdd(&sh.cand_n, 1u)] = v;
+            else if (b < bin) below = fmax(below, v);
+        });
         below = wave_max(below);
         if (lane == 0) sh.red[wave][0] = below;
         __syncthreads();
@@ -281,11 +303,12 @@ __device__ __forceinline__ double bilerp_win(const uint8_t* win, int ww, int ox,
     return (y2 - y) * a + (y - y1) * b;
 }
 
+// ww x ww window of an image plane (row pitch W) starting at (ox, oy) -> dst, by the lpf lanes of a group
 __device__ __forceinline__ void stage_window(uint8_t* dst, const uint8_t* img, int W, int H, int ox, int oy, int ww,
-                                             int sub, int lpf) {
+                                             uint32_t mww, int sub, int lpf) {
     const int64_t plane = (int64_t)W * H;
     for (int i = sub; i < ww * ww; i += lpf) {
-        const int ry = i / ww, rx = i - ry * ww;
+        const int ry = (int)udiv((uint32_t)i, mww), rx = i - ry * ww;
         const int64_t lin = (int64_t)(oy + ry) * W + (ox + rx);
         dst[i] = (lin >= 0 && lin < plane) ? img[lin] : (uint8_t)0;
     }
@@ -341,20 +364,27 @@ __device__ __attribute__((noinline)) void lm_step(Shared& sh, svo_level_trace& t
 #define SVO_STAMP(i) \
     if (kStamps && tid == 0) a.stamps[((int64_t)pair * (a.max_level + 1) + level) * 8 + (i)] = __builtin_amdgcn_s_memtime()
 
-template <bool kStamps>
+// kHalf: patch half size as a compile-time constant (the reference's patch p has h = p / 2 and a
+// (2h+1)^2 footprint); the launcher instantiates h = 0..9.
+template <int kHalf, bool kStamps>
 __global__ void __launch_bounds__(kThreads, 4) align_pairs_kernel(AlignArgs a) {
     __shared__ Shared sh;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int pair = blockIdx.x;
     const PairDesc& P = a.pairs[pair];
     const int nf = P.n_ref + P.n_kf;
-    const int A = a.area, h = a.half, side = 2 * a.half + 1;
+    constexpr int h = kHalf, side = 2 * kHalf + 1, A = side * side;
     const int M = nf * A;
-    // lane groups: lpf lanes per feature, fpw features per wave
-    const int lpf = A <= 16 ? 16 : (A <= 32 ? 32 : 64);
-    const int fpw = 64 / lpf;
+    // lane groups: lpf lanes per feature, fpw features per wave, U groups per wave iteration
+    constexpr int lpf = A <= 16 ? 16 : (A <= 32 ? 32 : 64);
+    constexpr int fpw = 64 / lpf;
     const int sub = lane & (lpf - 1), slotw = lane / lpf;
-    const int RW = 2 * h + 5, CW = 2 * h + 3, wbytes = RW * RW + CW * CW;
+    constexpr int RW = 2 * h + 5, CW = 2 * h + 3, wbytes = RW * RW + CW * CW;
+    constexpr int U = kUnroll < kWinBytes / (fpw * wbytes) ? kUnroll : kWinBytes / (fpw * wbytes);
+    static_assert(U >= 1, "staging buffer too small for this patch size");
+    const int ngroups = (nf + fpw - 1) / fpw;
+    const uint32_t mside = magic_of((uint32_t)side), mrw = magic_of((uint32_t)RW), mcw = magic_of((uint32_t)CW);
+    const int ky0 = sub / side - h, kx0 = sub % side - h;
     const int64_t fbase = (int64_t)pair * a.max_f;
     const double* __restrict__ px = a.px + 2 * fbase;
     const double* __restrict__ bearing = a.bearing + 3 * fbase;
@@ -363,10 +393,10 @@ __global__ void __launch_bounds__(kThreads, 4) align_pairs_kernel(AlignArgs a) {
     double* __restrict__ xw = a.xw + 3 * fbase;
     double* __restrict__ jimg = a.jimg + 12 * fbase;
     double* __restrict__ cuv = a.cuv + 2 * fbase;
+    double* __restrict__ fsum = a.fsum + 5 * fbase;
     uint8_t* __restrict__ fvis = a.fvis + fbase;
     double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
     svo_level_trace* traces = a.traces + (int64_t)pair * (a.max_level + 1);
-    uint8_t* wbuf = sh.win[wave] + slotw * wbytes;
 
     if (tid == 0) sh.pose = se3_load(P.cur_pose);
     for (int l = tid; l <= a.max_level; l += kThreads) {
@@ -399,13 +429,14 @@ __global__ void __launch_bounds__(kThreads, 4) align_pairs_kernel(AlignArgs a) {
             xw[3 * f] = pw.x; xw[3 * f + 1] = pw.y; xw[3 * f + 2] = pw.z;
         }
     }
+    if (tid == 0 && (M & 1)) res[M] = __builtin_inf();  // pad for the 16-B sweeps
     __syncthreads();
 
     double err = 0.0;
     int32_t status = kFailed;
     for (int level = a.max_level; level >= a.min_level; --level) {
-        const int32_t W = a.geom.w[level], H = a.geom.h[level];
         SVO_STAMP(0);
+        const int32_t W = a.geom.w[level], H = a.geom.h[level];
         const int64_t loff = a.geom.off[level];
         const uint8_t* __restrict__ ref_img = P.ref_pyr + loff;
         const uint8_t* __restrict__ kf_img = P.kf_pyr + loff;
@@ -452,40 +483,51 @@ __global__ void __launch_bounds__(kThreads, 4) align_pairs_kernel(AlignArgs a) {
         }
         for (int i = tid; i < kBins; i += kThreads) sh.hist[i] = 0;
         __syncthreads();
-        SVO_STAMP(1);
         const uint32_t n = sh.ired[0][2] * (uint32_t)A;
+        SVO_STAMP(1);
 
         // ---- S1: residuals through LDS-staged windows; value-bin histogram of r
-        for (int g = wave; g * fpw < nf; g += kWaves) {
-            const int f = g * fpw + slotw;
-            const bool fv = f < nf && fvis[f] == 3;
-            double ur = 0, vr = 0, cu = 0, cv = 0;
-            int rox = 0, roy = 0, cox = 0, coy = 0;
-            if (fv) {
-                ur = px[2 * f] * scale; vr = px[2 * f + 1] * scale;
-                cu = cuv[2 * f]; cv = cuv[2 * f + 1];
-                rox = (int)floor(ur) - h - 1; roy = (int)floor(vr) - h - 1;
-                cox = (int)floor(cu) - h; coy = (int)floor(cv) - h;
-                stage_window(wbuf, f < P.n_ref ? ref_img : kf_img, W, H, rox, roy, RW, sub, lpf);
-                stage_window(wbuf + RW * RW, cur_img, W, H, cox, coy, CW, sub, lpf);
+        for (int g0 = wave * U; g0 < ngroups; g0 += kWaves * U) {
+            int f[kUnroll], rox[kUnroll], roy[kUnroll], cox[kUnroll], coy[kUnroll];
+            double ur[kUnroll], vr[kUnroll], cu[kUnroll], cv[kUnroll];
+            bool fv[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                f[u] = (g0 + u) * fpw + slotw;
+                fv[u] = u < U && g0 + u < ngroups && f[u] < nf && fvis[f[u]] == 3;
+                if (fv[u]) {
+                    ur[u] = px[2 * f[u]] * scale; vr[u] = px[2 * f[u] + 1] * scale;
+                    cu[u] = cuv[2 * f[u]]; cv[u] = cuv[2 * f[u] + 1];
+                    rox[u] = (int)floor(ur[u]) - h - 1; roy[u] = (int)floor(vr[u]) - h - 1;
+                    cox[u] = (int)floor(cu[u]) - h; coy[u] = (int)floor(cv[u]) - h;
+                }
             }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+                if (fv[u]) {
+                    uint8_t* wb = sh.win[wave] + (u * fpw + slotw) * wbytes;
+                    stage_window(wb, f[u] < P.n_ref ? ref_img : kf_img, W, H, rox[u], roy[u], RW, mrw, sub, lpf);
+                    stage_window(wb + RW * RW, cur_img, W, H, cox[u], coy[u], CW, mcw, sub, lpf);
+                }
             wave_lds_sync();
-            if (f < nf) {
-                for (int k = sub; k < A; k += lpf) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                if (!(u < U && g0 + u < ngroups && f[u] < nf)) continue;
+                const uint8_t* wb = sh.win[wave] + (u * fpw + slotw) * wbytes;
+                for (int k = sub, ky = ky0, kx = kx0; k < A; k += lpf) {
+                    if (k != sub) { ky = (int)udiv((uint32_t)k, mside); kx = k - ky * side - h; ky -= h; }
                     double r = __builtin_inf();
-                    if (fv) {
-                        const int ky = k / side - h, kx = k - (k / side) * side - h;
-                        const double T = bilerp_win(wbuf, RW, rox, roy, ur + kx, vr + ky);
-                        const double I = bilerp_win(wbuf + RW * RW, CW, cox, coy, cu + kx, cv + ky);
+                    if (fv[u]) {
+                        const double T = bilerp_win(wb, RW, rox[u], roy[u], ur[u] + kx, vr[u] + ky);
+                        const double I = bilerp_win(wb + RW * RW, CW, cox[u], coy[u], cu[u] + kx, cv[u] + ky);
                         r = I - T;
                         atomicAdd(&sh.hist[sel_bin<false>(r)], 1u);
                     }
-                    res[f * A + k] = r;
+                    res[f[u] * A + k] = r;
                 }
             }
             wave_lds_sync();
         }
-        if (tid == 0 && (M & 1)) res[M] = __builtin_inf();  // pad for the double2 sweeps
         __syncthreads();
         SVO_STAMP(2);
 
@@ -499,84 +541,123 @@ __global__ void __launch_bounds__(kThreads, 4) align_pairs_kernel(AlignArgs a) {
             SVO_STAMP(3);
             for (int i = tid; i < kBins; i += kThreads) sh.hist[i] = 0;
             __syncthreads();
-            for (int s2 = 2 * tid; s2 < M; s2 += 2 * kThreads) {
-                const double2 rr = *reinterpret_cast<const double2*>(res + s2);
-                if (rr.x != __builtin_inf()) atomicAdd(&sh.hist[sel_bin<true>(fabs(rr.x - med))], 1u);
-                if (s2 + 1 < M && rr.y != __builtin_inf()) atomicAdd(&sh.hist[sel_bin<true>(fabs(rr.y - med))], 1u);
-            }
+            sweep_res(res, M, [&](double r) { atomicAdd(&sh.hist[sel_bin<true>(fabs(r - med))], 1u); });
             __syncthreads();
             mad = block_median<true>(sh, res, M, n, med);
         }
-        SVO_STAMP(4);
         double sigma = 1.482602218505602 * mad;
         if (sigma <= 2.220446049250313e-16) sigma = 2.220446049250313e-16;
         const double c = 4.6851 * sigma, c2 = c * c;
+        SVO_STAMP(4);
 
-        // ---- S5: Tukey weights, chi2, factorised normal equations (lower triangle)
+        // ---- S5: Tukey weights, chi2, per-feature factorised sums
         double chi_acc = 0.0;
-        if (lane < 28) sh.accw[wave][lane] = 0.0;
-        wave_lds_sync();
-        for (int g = wave; g * fpw < nf; g += kWaves) {
-            const int f = g * fpw + slotw;
-            const bool fv = f < nf && fvis[f] == 3;
-            double ur = 0, vr = 0;
-            int rox = 0, roy = 0;
-            if (fv) {
-                ur = px[2 * f] * scale; vr = px[2 * f + 1] * scale;
-                rox = (int)floor(ur) - h - 1; roy = (int)floor(vr) - h - 1;
-                stage_window(wbuf, f < P.n_ref ? ref_img : kf_img, W, H, rox, roy, RW, sub, lpf);
+        for (int g0 = wave * U; g0 < ngroups; g0 += kWaves * U) {
+            int f[kUnroll], rox[kUnroll], roy[kUnroll];
+            double ur[kUnroll], vr[kUnroll], r0[kUnroll];
+            bool fv[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                f[u] = (g0 + u) * fpw + slotw;
+                fv[u] = u < U && g0 + u < ngroups && f[u] < nf && fvis[f[u]] == 3;
+                if (fv[u]) {
+                    ur[u] = px[2 * f[u]] * scale; vr[u] = px[2 * f[u] + 1] * scale;
+                    rox[u] = (int)floor(ur[u]) - h - 1; roy[u] = (int)floor(vr[u]) - h - 1;
+                    r0[u] = sub < A ? res[f[u] * A + sub] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u)
+                if (fv[u]) {
+                    uint8_t* wb = sh.win[wave] + (u * fpw + slotw) * wbytes;
+                    stage_window(wb, f[u] < P.n_ref ? ref_img : kf_img, W, H, rox[u], roy[u], RW, mrw, sub, lpf);
+                }
+            wave_lds_sync();
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                if (!(u < U && g0 + u < ngroups)) continue;  // wave-uniform: every lane joins the shuffles below
+                const uint8_t* wb = sh.win[wave] + (u * fpw + slotw) * wbytes;
+                double sxx = 0, sxy = 0, syy = 0, sxr = 0, syr = 0;
+                if (fv[u]) {
+                    for (int k = sub, ky = ky0, kx = kx0; k < A; k += lpf) {
+                        double r = r0[u];
+                        if (k != sub) {
+                            ky = (int)udiv((uint32_t)k, mside); kx = k - ky * side - h; ky -= h;
+                            r = res[f[u] * A + k];
+                        }
+                        double w = 0.0;
+                        if (fabs(r) <= c) {
+                            const double t = 1.0 - (r * r) / c2;
+                            w = t * t;
+                        }
+                        chi_acc += r * r * w;
+                        if (w == 0.0) continue;
+                        const double row = vr[u] + ky, col = ur[u] + kx;
+                        const double dx = 0.5 * (bilerp_win(wb, RW, rox[u], roy[u], col + 1, row) -
+                                                 bilerp_win(wb, RW, rox[u], roy[u], col - 1, row));
+                        const double dy = 0.5 * (bilerp_win(wb, RW, rox[u], roy[u], col, row + 1) -
+                                                 bilerp_win(wb, RW, rox[u], roy[u], col, row - 1));
+                        const double wdx = w * dx, wdy = w * dy;
+                        sxx += wdx * dx; sxy += wdx * dy; syy += wdy * dy; sxr += wdx * r; syr += wdy * r;
+                    }
+                }
+                for (int o = lpf >> 1; o > 0; o >>= 1) {
+                    sxx += __shfl_down(sxx, o, lpf); sxy += __shfl_down(sxy, o, lpf); syy += __shfl_down(syy, o, lpf);
+                    sxr += __shfl_down(sxr, o, lpf); syr += __shfl_down(syr, o, lpf);
+                }
+                if (fv[u] && sub == 0) {
+                    double* fs = fsum + 5 * f[u];
+                    fs[0] = sxx; fs[1] = sxy; fs[2] = syy; fs[3] = sxr; fs[4] = syr;
+                }
             }
             wave_lds_sync();
-            double sxx = 0, sxy = 0, syy = 0, sxr = 0, syr = 0;
-            if (fv) {
-                for (int k = sub; k < A; k += lpf) {
-                    const double r = res[f * A + k];
-                    double w = 0.0;
-                    if (fabs(r) <= c) {
-                        const double t = 1.0 - (r * r) / c2;
-                        w = t * t;
-                    }
-                    chi_acc += r * r * w;
-                    if (w == 0.0) continue;
-                    const int ky = k / side - h, kx = k - (k / side) * side - h;
-                    const double row = vr + ky, col = ur + kx;
-                    const double dx = 0.5 * (bilerp_win(wbuf, RW, rox, roy, col + 1, row) -
-                                             bilerp_win(wbuf, RW, rox, roy, col - 1, row));
-                    const double dy = 0.5 * (bilerp_win(wbuf, RW, rox, roy, col, row + 1) -
-                                             bilerp_win(wbuf, RW, rox, roy, col, row - 1));
-                    const double wdx = w * dx, wdy = w * dy;
-                    sxx += wdx * dx; sxy += wdx * dy; syy += wdy * dy; sxr += wdx * r; syr += wdy * r;
-                }
-            }
-            for (int o = lpf >> 1; o > 0; o >>= 1) {
-                sxx += __shfl_down(sxx, o, lpf); sxy += __shfl_down(sxy, o, lpf); syy += __shfl_down(syy, o, lpf);
-                sxr += __shfl_down(sxr, o, lpf); syr += __shfl_down(syr, o, lpf);
-            }
-            for (int j = 0; j < fpw; ++j) {  // the wave's features one after another: fixed order
-                if (fv && sub == 0 && slotw == j) {
-                    double ja[6], jb[6];
-                    for (int t = 0; t < 6; ++t) { ja[t] = jimg[12 * f + t]; jb[t] = jimg[12 * f + 6 + t]; }
-                    double* acc = sh.accw[wave];
-                    int q = 0;
-                    for (int i = 0; i < 6; ++i) {
-                        for (int t = 0; t <= i; ++t)
-                            acc[q++] += ja[i] * ja[t] * sxx + (ja[i] * jb[t] + jb[i] * ja[t]) * sxy + jb[i] * jb[t] * syy;
-                        acc[21 + i] += ja[i] * sxr + jb[i] * syr;
-                    }
-                }
-                wave_lds_sync();
-            }
         }
         chi_acc = wave_sum(chi_acc);
         if (lane == 0) sh.accw[wave][27] = chi_acc;
         __syncthreads();
+
+        // ---- P5b: expand the per-feature sums into J^T W J (lower) and J^T W r.  Thread (term, chunk):
+        // 27 terms x 16 feature chunks, one accumulator each; chunks summed in a fixed order below.
+        {
+            const int term = tid & 31, chunk = tid >> 5;
+            if (term < 27) {
+                int i, j;  // term -> (i, j) of the lower triangle, or g_i for term >= 21
+                if (term < 21) {
+                    i = 0;
+                    while ((i + 1) * (i + 2) / 2 <= term) ++i;
+                    j = term - i * (i + 1) / 2;
+                } else {
+                    i = term - 21;
+                    j = 0;
+                }
+                double acc = 0.0;
+                for (int f = chunk; f < nf; f += kThreads / 32) {
+                    if (fvis[f] != 3) continue;
+                    const double* fs = fsum + 5 * f;
+                    const double* J = jimg + 12 * f;
+                    const double ai = J[i], bi = J[6 + i];
+                    if (term < 21) {
+                        const double aj = J[j], bj = J[6 + j];
+                        acc += ai * aj * fs[0] + (ai * bj + bi * aj) * fs[1] + bi * bj * fs[2];
+                    } else {
+                        acc += ai * fs[3] + bi * fs[4];
+                    }
+                }
+                sh.part[chunk][term] = acc;
+            }
+        }
+        __syncthreads();
         SVO_STAMP(5);
 
         // ---- P6: damped step, solve, update (one lane; LDS workspace)
-        if (tid < 28) {  // wave partials in a fixed order
+        if (tid < 27) {  // chunk partials in a fixed order
             double s = 0.0;
-            for (int w = 0; w < kWaves; ++w) s += sh.accw[w][tid];
+            for (int c = 0; c < kThreads / 32; ++c) s += sh.part[c][tid];
             sh.tot[tid] = s;
+        } else if (tid == 27) {
+            double s = 0.0;
+            for (int w = 0; w < kWaves; ++w) s += sh.accw[w][27];
+            sh.tot[27] = s;
         }
         __syncthreads();
         if (tid == 0) lm_step(sh, traces[level], n, med, mad, sigma);
@@ -593,11 +674,27 @@ __global__ void __launch_bounds__(kThreads, 4) align_pairs_kernel(AlignArgs a) {
     }
 }
 
-void launch_align(const AlignArgs& a, hipStream_t s) {
+template <int kHalf>
+static void launch_h(const AlignArgs& a, hipStream_t s) {
     if (a.stamps)
-        hipLaunchKernelGGL(align_pairs_kernel<true>, dim3(a.n_pairs), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((align_pairs_kernel<kHalf, true>), dim3(a.n_pairs), dim3(kThreads), 0, s, a);
     else
-        hipLaunchKernelGGL(align_pairs_kernel<false>, dim3(a.n_pairs), dim3(kThreads), 0, s, a);
+        hipLaunchKernelGGL((align_pairs_kernel<kHalf, false>), dim3(a.n_pairs), dim3(kThreads), 0, s, a);
+}
+
+void launch_align(const AlignArgs& a, hipStream_t s) {
+    switch (a.half) {
+        case 0: launch_h<0>(a, s); break;
+        case 1: launch_h<1>(a, s); break;
+        case 2: launch_h<2>(a, s); break;
+        case 3: launch_h<3>(a, s); break;
+        case 4: launch_h<4>(a, s); break;
+        case 5: launch_h<5>(a, s); break;
+        case 6: launch_h<6>(a, s); break;
+        case 7: launch_h<7>(a, s); break;
+        case 8: launch_h<8>(a, s); break;
+        default: launch_h<9>(a, s); break;  // capi rejects larger patches (align_window_bytes)
+    }
 }
 
 int align_window_bytes(int half) {

@@ -73,7 +73,7 @@ struct svo_align_batch {
     std::vector<svo::PairDesc> h_pairs;
     std::vector<uint8_t> pair_set;
     svo::PairDesc* d_pairs;
-    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_cuv, *d_res, *d_pose_out, *d_err;
+    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_cuv, *d_fsum, *d_res, *d_pose_out, *d_err;
     uint8_t *d_has_point, *d_fvis;
     int32_t* d_status;
     svo_level_trace* d_traces;
@@ -236,7 +236,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_jimg,
-                    b->d_cuv, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces, b->d_stamps};
+                    b->d_cuv, b->d_fsum, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces, b->d_stamps};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -272,6 +272,7 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_xw, F * 3 * sizeof(double));
     ALLOC(b->d_jimg, F * 12 * sizeof(double));
     ALLOC(b->d_cuv, F * 2 * sizeof(double));
+    ALLOC(b->d_fsum, F * 5 * sizeof(double));
     ALLOC(b->d_fvis, F);
     b->res_stride = ((int64_t)max_features * area + 2 + 63) / 64 * 64;
     ALLOC(b->d_res, (size_t)n_pairs * b->res_stride * sizeof(double));
@@ -367,7 +368,7 @@ int svo_align_batch_run(svo_align_batch* b) {
     svo::AlignArgs a;
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
-    a.xw = b->d_xw; a.jimg = b->d_jimg; a.cuv = b->d_cuv; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
+    a.xw = b->d_xw; a.jimg = b->d_jimg; a.cuv = b->d_cuv; a.fsum = b->d_fsum; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
     a.stamps = b->d_stamps;
     a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;

@@ -36,6 +36,7 @@ struct AlignArgs {
     double* jimg;             // scratch [n_pairs*max_f][12]  image Jacobian at the current level
     double* cuv;              // scratch [n_pairs*max_f][2]   projection into cur at the current level
     uint8_t* fvis;            // scratch [n_pairs*max_f]      bit0 ref visible, bit1 cur visible
+    double* fsum;             // scratch [n_pairs*max_f][5]   per-feature S_xx S_xy S_yy S_xr S_yr
     double* res;              // scratch [n_pairs][res_stride] residual per pixel slot (+inf = invisible)
     int64_t res_stride;       // >= max_f*area + 1, even (16-B aligned rows for the double2 sweeps)
     double* pose_out;         // [n_pairs][7]
