@@ -145,10 +145,6 @@ int svo_align_batch_run(svo_align_batch* batch);
 int svo_align_batch_results(svo_align_batch* batch, double* poses, double* err, int32_t* status);
 /* Per-level records of one pair (max_level+1 entries, indexed by level). */
 int svo_align_batch_traces(svo_align_batch* batch, int32_t pair, svo_level_trace* out);
-/* Diagnostics: when the batch was created with SVO_PHASE_STAMPS=1 in the environment, the kernel
- * records the shader clock (s_memtime) at 8 phase boundaries per pair and level; copies
- * n_pairs*(max_level+1)*8 values.  Returns SVO_ERR_STATE when stamps were not enabled. */
-int svo_align_batch_phase_stamps(svo_align_batch* batch, uint64_t* out);
 
 /* ---------------------------------------------------------------- FeatureAlignment
  * Replaces FeatureAlignment::align(refFeature, curFrame, pixelPos) (src/feature_alignment.cpp:25-62,

@@ -64,7 +64,6 @@ _SIGNATURES = [
     ("svo_align_batch_run", c_int32, [c_void_p]),
     ("svo_align_batch_results", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     ("svo_align_batch_traces", c_int32, [c_void_p, c_int32, c_void_p]),
-    ("svo_align_batch_phase_stamps", c_int32, [c_void_p, c_void_p]),
     ("svo_feature_align", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_int32,
                                     c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
 ]

@@ -291,12 +291,6 @@ class AlignBatch:
         check(lib().svo_align_batch_traces(self.handle, int(pair), ctypes.cast(out, ctypes.c_void_p)))
         return out
 
-    def phase_stamps(self):
-        """s_memtime per (pair, level, phase) — needs SVO_PHASE_STAMPS=1 when the batch was created."""
-        out = np.zeros((self.n_pairs, self.max_level + 1, 8), np.uint64)
-        check(lib().svo_align_batch_phase_stamps(self.handle, ptr(out)))
-        return out
-
     def close(self):
         if getattr(self, "handle", None):
             lib().svo_align_batch_destroy(self.handle)

@@ -73,11 +73,11 @@ struct svo_align_batch {
     std::vector<svo::PairDesc> h_pairs;
     std::vector<uint8_t> pair_set;
     svo::PairDesc* d_pairs;
-    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_cuv, *d_fsum, *d_res, *d_pose_out, *d_err;
+    svo::PairState* d_state;
+    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_fsum, *d_res, *d_pose_out, *d_err;
     uint8_t *d_has_point, *d_fvis;
     int32_t* d_status;
     svo_level_trace* d_traces;
-    unsigned long long* d_stamps;  // SVO_PHASE_STAMPS=1 diagnostics
     bool ran;
 };
 
@@ -236,7 +236,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_jimg,
-                    b->d_cuv, b->d_fsum, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces, b->d_stamps};
+                    b->d_state, b->d_fsum, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -246,7 +246,7 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     if (!c || !cam || !prm || !out) return fail(SVO_ERR_ARG, "null argument");
     *out = nullptr;
     if (n_pairs <= 0 || max_features <= 0) return fail(SVO_ERR_ARG, "n_pairs and max_features must be > 0");
-    if (prm->patch_size < 1 || svo::align_window_bytes(prm->patch_size / 2) > svo::align_window_capacity())
+    if (prm->patch_size < 1 || prm->patch_size / 2 > svo::align_max_half())
         return fail(SVO_ERR_ARG, "patch_size %d unsupported (<= 19)", prm->patch_size);
     if (prm->min_level < 0 || prm->max_level < prm->min_level || prm->max_level >= svo::kMaxLevels)
         return fail(SVO_ERR_ARG, "bad level range [%d,%d]", prm->min_level, prm->max_level);
@@ -271,8 +271,8 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_has_point, F);
     ALLOC(b->d_xw, F * 3 * sizeof(double));
     ALLOC(b->d_jimg, F * 12 * sizeof(double));
-    ALLOC(b->d_cuv, F * 2 * sizeof(double));
-    ALLOC(b->d_fsum, F * 5 * sizeof(double));
+    ALLOC(b->d_state, sizeof(svo::PairState) * n_pairs);
+    ALLOC(b->d_fsum, F * 6 * sizeof(double));
     ALLOC(b->d_fvis, F);
     b->res_stride = ((int64_t)max_features * area + 2 + 63) / 64 * 64;
     ALLOC(b->d_res, (size_t)n_pairs * b->res_stride * sizeof(double));
@@ -280,8 +280,6 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_err, (size_t)n_pairs * sizeof(double));
     ALLOC(b->d_status, (size_t)n_pairs * sizeof(int32_t));
     ALLOC(b->d_traces, (size_t)n_pairs * (prm->max_level + 1) * sizeof(svo_level_trace));
-    { const char* env = getenv("SVO_PHASE_STAMPS");
-      if (env && env[0] == '1') ALLOC(b->d_stamps, (size_t)n_pairs * (prm->max_level + 1) * 8 * sizeof(unsigned long long)); }
 #undef ALLOC
     if (e != hipSuccess) {
         free_batch(b);
@@ -368,9 +366,8 @@ int svo_align_batch_run(svo_align_batch* b) {
     svo::AlignArgs a;
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
-    a.xw = b->d_xw; a.jimg = b->d_jimg; a.cuv = b->d_cuv; a.fsum = b->d_fsum; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
+    a.xw = b->d_xw; a.jimg = b->d_jimg; a.state = b->d_state; a.fsum = b->d_fsum; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
-    a.stamps = b->d_stamps;
     a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
     a.min_level = b->params.min_level; a.max_level = b->params.max_level;
     a.fx = b->cam.fx; a.fy = b->cam.fy; a.cx = b->cam.cx; a.cy = b->cam.cy;
@@ -465,14 +462,3 @@ int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, con
 }
 
 }  // extern "C"
-
-extern "C" int svo_align_batch_phase_stamps(svo_align_batch* b, uint64_t* out) {
-    if (!b || !out) return fail(SVO_ERR_ARG, "null argument");
-    if (!b->d_stamps) return fail(SVO_ERR_STATE, "batch created without SVO_PHASE_STAMPS=1");
-    if (!b->ran) return fail(SVO_ERR_STATE, "batch has not been run");
-    SVO_HIP(hipSetDevice(b->ctx->device));
-    const size_t cnt = (size_t)b->n_pairs * (b->params.max_level + 1) * 8;
-    SVO_HIP(hipMemcpyAsync(out, b->d_stamps, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, b->ctx->stream));
-    SVO_HIP(hipStreamSynchronize(b->ctx->stream));
-    return SVO_OK;
-}

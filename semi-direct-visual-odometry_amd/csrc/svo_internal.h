@@ -16,7 +16,7 @@ struct LevelGeom {  // one pyramid geometry (all frames of a set share it)
     int32_t levels;
 };
 
-struct PairDesc {  // per frame pair, device resident
+struct PairDesc {  // per frame pair, device resident (inputs; never written by the kernels)
     const uint8_t* ref_pyr;
     const uint8_t* kf_pyr;
     const uint8_t* cur_pyr;
@@ -26,32 +26,38 @@ struct PairDesc {  // per frame pair, device resident
     int32_t n_ref, n_kf;
 };
 
+struct PairState {  // per frame pair, carried from stage to stage and level to level
+    double pose[7];             // current estimate of cur->m_absPose
+    double med, mad, sigma, c;  // robust scale of the current level (K2)
+    double err;                 // RMSE of the last finished level
+    uint32_t n, n_ref_vis;      // visible pixel slots / ref-visible features of the current level
+    int32_t status, active;     // Optimizer::Status of the last level; 0 = nothing to align
+};
+
 struct AlignArgs {
     const PairDesc* pairs;
+    PairState* state;         // [n_pairs]
     const double* px;         // [n_pairs*max_f][2]
     const double* bearing;    // [n_pairs*max_f][3]
     const double* point;      // [n_pairs*max_f][3]
     const uint8_t* has_point; // [n_pairs*max_f]
     double* xw;               // scratch [n_pairs*max_f][3]   world point per feature
     double* jimg;             // scratch [n_pairs*max_f][12]  image Jacobian at the current level
-    double* cuv;              // scratch [n_pairs*max_f][2]   projection into cur at the current level
     uint8_t* fvis;            // scratch [n_pairs*max_f]      bit0 ref visible, bit1 cur visible
-    double* fsum;             // scratch [n_pairs*max_f][5]   per-feature S_xx S_xy S_yy S_xr S_yr
+    double* fsum;             // scratch [n_pairs*max_f][6]   S_xx S_xy S_yy S_xr S_yr chi2 per feature
     double* res;              // scratch [n_pairs][res_stride] residual per pixel slot (+inf = invisible)
-    int64_t res_stride;       // >= max_f*area + 1, even (16-B aligned rows for the double2 sweeps)
+    int64_t res_stride;       // >= max_f*area + 1, even (16-B aligned rows for the 16-B sweeps)
     double* pose_out;         // [n_pairs][7]
     double* err_out;          // [n_pairs]
     int32_t* status_out;      // [n_pairs]
     svo_level_trace* traces;  // [n_pairs][max_level+1]
-    unsigned long long* stamps;  // diagnostics: [n_pairs][max_level+1][8] s_memtime per phase, or null
     int32_t n_pairs, max_f, half, area, min_level, max_level;
     double fx, fy, cx, cy;
     LevelGeom geom;
 };
 
 void launch_align(const AlignArgs& a, hipStream_t s);
-int align_window_bytes(int half);  // LDS staging bytes one wave needs for this half patch size
-int align_window_capacity();       // LDS staging bytes available per wave
+int align_max_half();  // largest patch half size the alignment kernels are instantiated for
 void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t count, hipStream_t s);
 
 struct FeatureAlignArgs {

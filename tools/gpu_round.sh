@@ -22,7 +22,6 @@ for step in "$@"; do
         tests) run tests 900 python3 -m pytest tests -q -m gpu -p no:cacheprovider ;;
         bench) run bench 600 python3 bench.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu ;;
-        phase) run phase 300 python3 tools/phase_profile.py ;;
         pmc) run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu ;;
         *) echo "unknown step $step" ;;
     esac
