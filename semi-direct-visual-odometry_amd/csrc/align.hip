@@ -1,26 +1,28 @@
 // align.hip — sparse image alignment (ImageAlignment::align, src/image_alignment.cpp:25-67) on gfx950.
 //
-// A batch holds n_pairs independent frame pairs.  The coarse-to-fine chain is run as
-// stage kernels, all pairs of the batch at once, enqueued back to back on the context stream (and
-// captured into a hipGraph by the C ABI): every stage gets its own register budget and launch shape.
+// A batch holds n_pairs independent frame pairs.  The coarse-to-fine chain runs as
+// stage kernels over all pairs of the batch, enqueued back to back on the context stream: each stage
+// has its own register budget and launch shape (one persistent kernel spilled ~20 GB/launch).
 //   K0 init      thread / feature : X_w = T_f^-1 (bearing * |P - C_f|) (:153-155); per-pair state
 //   per level (max..min):
 //   K1 residual  lane group / feature (32 lanes for the 25 px of patch 5, 64 for patch 7): ref
 //                visibility (border rule :140-149), projection pose*X_w into cur (:320-340), image
-//                Jacobian at the WORLD point (:163, :194-248); the ref window ((2h+5)^2 px) and cur
-//                window ((2h+3)^2 px) are staged in LDS with a few byte loads, then each lane samples
-//                its pixel: r = I_cur - T_ref (:359) -> per-pair residual row (+inf = invisible slot)
-//   K2 scale     one workgroup / pair: exact median of the visible r (src/algorithm.cpp:834-853) and
-//                of |r - median| (MAD, :855-865) -> sigma = 1.482602218505602 * MAD (:867-872).
-//                Values are binned by a monotone map into an LDS histogram; the bin of rank n/2 is
-//                exact, one sweep gathers that bin's values into LDS and ranks them exactly; an
-//                overfull bin falls back to an 11-bit radix select on order-preserving keys
+//                Jacobian at the WORLD point (:163, :194-248).  The ref window ((2h+5)^2 px) and the
+//                cur window ((2h+3)^2 px) are staged in LDS one row per lane with two aligned 16-B
+//                loads; each lane then samples its pixel: r = I_cur - T_ref (:359) -> per-pair
+//                residual row (+inf = invisible slot)
+//   K2 scale     one workgroup / pair: exact median of the visible r (src/algorithm.cpp:834-853) and of
+//                |r - median| (MAD, :855-865) -> sigma = 1.482602218505602 * MAD (:867-872).  Values
+//                are binned by a monotone map into an LDS histogram; the bin of rank n/2 is exact; one
+//                sweep gathers that bin's values into LDS and ranks them exactly; an overfull bin falls
+//                back to an 11-bit radix select on order-preserving keys
 //   K3 weights   lane group / feature: Tukey weight (src/optimizer.cpp:485-514), chi2 term, dx/dy
-//                re-sampled from the staged ref window, per-feature sums S_xx S_xy S_yy S_xr S_yr
-//   K4 solve     one workgroup / pair: expand the sums with the 2x6 image Jacobian into the lower
-//                triangle of J^T W J and J^T W r (factorised J row = dx*Jimg0 + dy*Jimg1) with fixed
-//                summation order (deterministic, no float atomics); one lane: Nielsen damping,
-//                Eigen-LDLT, pose <- pose * exp(-dx), status, RMSE (src/optimizer.cpp:279-366, :379)
+//                re-sampled from the staged ref window; per feature the 5 sums S_xx S_xy S_yy S_xr S_yr
+//                are expanded with the 2x6 image Jacobian (factorised J row = dx*Jimg0 + dy*Jimg1),
+//                one normal-equation term per lane, into per-workgroup partials (fixed order)
+//   K4 solve     one workgroup / pair: partials summed in a fixed order (deterministic, no float
+//                atomics); one lane: Nielsen damping, Eigen-LDLT, pose <- pose * exp(-dx), status,
+//                RMSE (src/optimizer.cpp:279-366, src/image_alignment.cpp:379)
 #include "svo_internal.h"
 #include "svo_math.h"
 
@@ -28,11 +30,10 @@ namespace svo {
 
 namespace {
 
-constexpr int kFeatThreads = 256;    // K1 / K3 workgroup
-constexpr int kFeatPerWave = 8;      // feature groups a K1/K3 wave walks through
+constexpr int kFeatThreads = 256;    // K1 / K3 workgroup (4 waves)
+constexpr int kFeatWaves = kFeatThreads / 64;
 constexpr int kSelThreads = 1024;    // K2 workgroup
 constexpr int kSelWaves = kSelThreads / 64;
-constexpr int kSolveThreads = 512;   // K4 workgroup
 constexpr int kBins = 4096;
 constexpr double kBinScale = 32.0;   // bins per grey level
 constexpr double kBinOffset = 64.0;  // signed map covers [-64, 64); outliers clamp to the end bins
@@ -59,42 +60,54 @@ __device__ __forceinline__ void wave_lds_sync() {  // this wave's LDS writes -> 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// bilinearInterpolationDouble (src/algorithm.cpp:896-905) reading a staged window whose top-left
-// image pixel is (ox, oy); cells past the image edge hold 0 and only ever carry a zero weight.
-__device__ __forceinline__ double bilerp_win(const uint8_t* win, int ww, int ox, int oy, double x, double y) {
-    const int32_t x1 = (int32_t)x, y1 = (int32_t)y, x2 = x1 + 1, y2 = y1 + 1;
-    const uint8_t* r1 = win + (y1 - oy) * ww - ox;
-    const uint8_t* r2 = r1 + ww;
-    const double a = (x2 - x) * r1[x1] + (x - x1) * r1[x2];
-    const double b = (x2 - x) * r2[x1] + (x - x1) * r2[x2];
-    return (y2 - y) * a + (y - y1) * b;
-}
-
-// ww x ww window of an image plane (row pitch W) starting at (ox, oy) -> dst, by the lpf lanes of a group
-template <int ww, int lpf>
-__device__ __forceinline__ void stage_window(uint8_t* dst, const uint8_t* img, int W, int H, int ox, int oy, int sub) {
-    const int64_t plane = (int64_t)W * H;
-#pragma unroll
-    for (int i0 = 0; i0 < ww * ww; i0 += lpf) {
-        const int i = i0 + sub;
-        if (i < ww * ww) {
-            const int ry = i / ww, rx = i - ry * ww;
-            const int64_t lin = (int64_t)(oy + ry) * W + (ox + rx);
-            dst[i] = (lin >= 0 && lin < plane) ? img[lin] : (uint8_t)0;
-        }
-    }
-}
-
 template <int kHalf>
 struct Geo {
     static constexpr int h = kHalf, side = 2 * kHalf + 1, A = side * side;
     static constexpr int lpf = A <= 16 ? 16 : (A <= 32 ? 32 : 64);  // lanes per feature
     static constexpr int fpw = 64 / lpf;                               // features per wave
     static constexpr int RW = 2 * h + 5, CW = 2 * h + 3;               // staged window sides
-    static constexpr int wbytes = RW * RW + CW * CW;
+    static constexpr int NB = (RW + 15 + 15) / 16;                     // 16-B blocks per staged row
+    static constexpr int pitch = NB * 16;                              // LDS bytes per staged row
+    static constexpr int rbytes = RW * pitch, cbytes = CW * pitch;
+    static constexpr int rounds = (28 + lpf - 1) / lpf;                // normal-equation terms per lane
+    static_assert(RW + CW <= lpf, "one lane per staged row");
 };
 
+// Stage rows [0, ww) of a window with top-left pixel (ox, oy) of an image plane (row pitch W, plane
+// 256-B aligned): lane `row` copies the NB aligned 16-B blocks covering [lin, lin + ww) of its row,
+// lin = (oy + row) * W + ox.  Bytes past the row end are the bytes the reference's unchecked Eigen map
+// would read (they only ever carry a zero bilinear weight).
+template <int ww, int NB>
+__device__ __forceinline__ void stage_rows(uint8_t* dst, const uint8_t* plane, int W, int ox, int oy, int row) {
+    if (row < ww) {
+        const int64_t lin = (int64_t)(oy + row) * W + ox;
+        const uint4* src = reinterpret_cast<const uint4*>(plane + (lin & ~(int64_t)15));
+        uint4* d = reinterpret_cast<uint4*>(dst + row * NB * 16);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) d[b] = src[b];
+    }
+}
+
+// bilinearInterpolationDouble (src/algorithm.cpp:896-905) on a window staged by stage_rows
+template <int NB>
+__device__ __forceinline__ double bilerp_staged(const uint8_t* st, int W, int ox, int oy, double x, double y) {
+    const int32_t x1 = (int32_t)x, y1 = (int32_t)y, x2 = x1 + 1, y2 = y1 + 1;
+    const int64_t lin1 = (int64_t)y1 * W + ox;
+    const uint8_t* r1 = st + (y1 - oy) * NB * 16 + (int)(lin1 & 15) - ox;
+    const uint8_t* r2 = st + (y1 + 1 - oy) * NB * 16 + (int)((lin1 + W) & 15) - ox;
+    const double a = (x2 - x) * r1[x1] + (x - x1) * r1[x2];
+    const double b = (x2 - x) * r2[x1] + (x - x1) * r2[x2];
+    return (y2 - y) * a + (y - y1) * b;
+}
+
 }  // namespace
+
+int align_chunks(int max_f, int half, int feat_iters) {
+    const int A = (2 * half + 1) * (2 * half + 1);
+    const int fpw = A <= 16 ? 4 : (A <= 32 ? 2 : 1);
+    const int fpc = kFeatWaves * fpw * feat_iters;
+    return (max_f + fpc - 1) / fpc;
+}
 
 // ------------------------------------------------------------------ K0: world points, pair state
 __global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
@@ -132,12 +145,12 @@ __global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
 }
 
 // ------------------------------------------------------------------ K1: visibility, projection, residuals
-// grid.x = n_pairs * chunks; a workgroup walks kFeatPerWave groups per wave of one pair's features.
+// grid.x = n_pairs * chunks; each wave walks feat_iters feature groups of one pair.
 template <int kHalf>
-__global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs a, int level, int chunks) {
+__global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs a, int level) {
     using G = Geo<kHalf>;
-    __shared__ uint8_t win[kFeatThreads / 64][G::fpw * G::wbytes];
-    const int pair = blockIdx.x / chunks, chunk = blockIdx.x - pair * chunks;
+    __shared__ __attribute__((aligned(16))) uint8_t win[kFeatWaves][G::fpw][G::rbytes + G::cbytes];
+    const int pair = blockIdx.x / a.chunks, chunk = blockIdx.x - pair * a.chunks;
     const PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
@@ -151,11 +164,13 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
     const SE3 pose = se3_load(S.pose);
     const int64_t fbase = (int64_t)pair * a.max_f;
     double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
-    uint8_t* wb = win[wave] + slotw * G::wbytes;
-    const int fpc = (kFeatThreads / 64) * kFeatPerWave * G::fpw;  // features per chunk
-    for (int it = 0; it < kFeatPerWave; ++it) {
-        const int f = chunk * fpc + (it * (kFeatThreads / 64) + wave) * G::fpw + slotw;
-        if (chunk * fpc + (it * (kFeatThreads / 64) + wave) * G::fpw >= nf) break;  // wave-uniform
+    uint8_t* wref = win[wave][slotw];
+    uint8_t* wcur = wref + G::rbytes;
+    const int fpc = kFeatWaves * G::fpw * a.feat_iters;  // features per chunk
+    for (int it = 0; it < a.feat_iters; ++it) {
+        const int f0 = chunk * fpc + (it * kFeatWaves + wave) * G::fpw;
+        if (f0 >= nf) break;  // wave-uniform
+        const int f = f0 + slotw;
         const int64_t gf = fbase + f;
         uint8_t vis = 0;
         double ur = 0, vr = 0, cu = 0, cv = 0;
@@ -184,8 +199,10 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
         const int rox = (int)floor(ur) - G::h - 1, roy = (int)floor(vr) - G::h - 1;
         const int cox = (int)floor(cu) - G::h, coy = (int)floor(cv) - G::h;
         if (vis == 3) {
-            stage_window<G::RW, G::lpf>(wb, (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff, W, H, rox, roy, sub);
-            stage_window<G::CW, G::lpf>(wb + G::RW * G::RW, P.cur_pyr + loff, W, H, cox, coy, sub);
+            if (sub < G::RW)
+                stage_rows<G::RW, G::NB>(wref, (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff, W, rox, roy, sub);
+            else
+                stage_rows<G::CW, G::NB>(wcur, P.cur_pyr + loff, W, cox, coy, sub - G::RW);
         }
         wave_lds_sync();
         if (f < nf) {
@@ -196,8 +213,8 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
                     const int ky = k / G::side - G::h, kx = k % G::side - G::h;
                     double r = __builtin_inf();
                     if (vis == 3) {
-                        const double T = bilerp_win(wb, G::RW, rox, roy, ur + kx, vr + ky);
-                        const double I = bilerp_win(wb + G::RW * G::RW, G::CW, cox, coy, cu + kx, cv + ky);
+                        const double T = bilerp_staged<G::NB>(wref, W, rox, roy, ur + kx, vr + ky);
+                        const double I = bilerp_staged<G::NB>(wcur, W, cox, coy, cu + kx, cv + ky);
                         r = I - T;
                     }
                     res[(int64_t)f * G::A + k] = r;
@@ -470,39 +487,59 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
     }
 }
 
-// ------------------------------------------------------------------ K3: weights, per-feature sums
+// ------------------------------------------------------------------ K3: weights, normal-equation partials
 template <int kHalf>
-__global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a, int level, int chunks) {
+__global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a, int level) {
     using G = Geo<kHalf>;
-    __shared__ uint8_t win[kFeatThreads / 64][G::fpw * G::RW * G::RW];
-    const int pair = blockIdx.x / chunks, chunk = blockIdx.x - pair * chunks;
+    __shared__ __attribute__((aligned(16))) uint8_t win[kFeatWaves][G::fpw][G::rbytes];
+    __shared__ double part[kFeatWaves][G::fpw][28];
+    const int pair = blockIdx.x / a.chunks, chunk = blockIdx.x - pair * a.chunks;
     const PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
     const int nf = P.n_ref + P.n_kf;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int sub = lane & (G::lpf - 1), slotw = lane / G::lpf;
-    const int W = a.geom.w[level], H = a.geom.h[level];
+    const int W = a.geom.w[level];
     const int64_t loff = a.geom.off[level];
     const double scale = 1.0 / (double)(1 << level);
     const double c = S.c, c2 = c * c;
     const int64_t fbase = (int64_t)pair * a.max_f;
     const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
-    uint8_t* wb = win[wave] + slotw * G::RW * G::RW;
-    const int fpc = (kFeatThreads / 64) * kFeatPerWave * G::fpw;
-    for (int it = 0; it < kFeatPerWave; ++it) {
-        const int f = chunk * fpc + (it * (kFeatThreads / 64) + wave) * G::fpw + slotw;
-        if (chunk * fpc + (it * (kFeatThreads / 64) + wave) * G::fpw >= nf) break;  // wave-uniform
+    uint8_t* wref = win[wave][slotw];
+    // the normal-equation terms this lane owns: t < 21 -> H(i, j) lower, t < 27 -> g(i), t == 27 -> chi2
+    int ti[G::rounds], tj[G::rounds];
+    double acc[G::rounds];
+#pragma unroll
+    for (int q = 0; q < G::rounds; ++q) {
+        const int t = sub + q * G::lpf;
+        int i = 0, j = 0;
+        if (t < 21) {
+            while ((i + 1) * (i + 2) / 2 <= t) ++i;
+            j = t - i * (i + 1) / 2;
+        } else if (t < 27) {
+            i = t - 21;
+        }
+        ti[q] = i;
+        tj[q] = j;
+        acc[q] = 0.0;
+    }
+    const int fpc = kFeatWaves * G::fpw * a.feat_iters;
+    for (int it = 0; it < a.feat_iters; ++it) {
+        const int f0 = chunk * fpc + (it * kFeatWaves + wave) * G::fpw;
+        if (f0 >= nf) break;  // wave-uniform
+        const int f = f0 + slotw;
         const int64_t gf = fbase + f;
         const bool fv = f < nf && a.fvis[gf] == 3;
-        double ur = 0, vr = 0;
+        double ur = 0, vr = 0, jv = 0.0;
         int rox = 0, roy = 0;
         if (fv) {
             ur = a.px[2 * gf] * scale;
             vr = a.px[2 * gf + 1] * scale;
             rox = (int)floor(ur) - G::h - 1;
             roy = (int)floor(vr) - G::h - 1;
-            stage_window<G::RW, G::lpf>(wb, (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff, W, H, rox, roy, sub);
+            stage_rows<G::RW, G::NB>(wref, (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff, W, rox, roy, sub);
+            if (sub < 12) jv = a.jimg[12 * gf + sub];
         }
         wave_lds_sync();
         double sxx = 0, sxy = 0, syy = 0, sxr = 0, syr = 0, chi = 0;
@@ -521,10 +558,10 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
                     chi += r * r * w;
                     if (w != 0.0) {
                         const double row = vr + ky, col = ur + kx;
-                        const double dx = 0.5 * (bilerp_win(wb, G::RW, rox, roy, col + 1, row) -
-                                                 bilerp_win(wb, G::RW, rox, roy, col - 1, row));
-                        const double dy = 0.5 * (bilerp_win(wb, G::RW, rox, roy, col, row + 1) -
-                                                 bilerp_win(wb, G::RW, rox, roy, col, row - 1));
+                        const double dx = 0.5 * (bilerp_staged<G::NB>(wref, W, rox, roy, col + 1, row) -
+                                                 bilerp_staged<G::NB>(wref, W, rox, roy, col - 1, row));
+                        const double dy = 0.5 * (bilerp_staged<G::NB>(wref, W, rox, roy, col, row + 1) -
+                                                 bilerp_staged<G::NB>(wref, W, rox, roy, col, row - 1));
                         const double wdx = w * dx, wdy = w * dy;
                         sxx += wdx * dx; sxy += wdx * dy; syy += wdy * dy; sxr += wdx * r; syr += wdy * r;
                     }
@@ -536,19 +573,39 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
             sxx += __shfl_down(sxx, o, G::lpf); sxy += __shfl_down(sxy, o, G::lpf); syy += __shfl_down(syy, o, G::lpf);
             sxr += __shfl_down(sxr, o, G::lpf); syr += __shfl_down(syr, o, G::lpf); chi += __shfl_down(chi, o, G::lpf);
         }
-        if (fv && sub == 0) {
-            double* fs = a.fsum + 6 * gf;
-            fs[0] = sxx; fs[1] = sxy; fs[2] = syy; fs[3] = sxr; fs[4] = syr; fs[5] = chi;
+        // every lane of the group gets the feature's sums and the Jimg entries of its terms
+        sxx = __shfl(sxx, 0, G::lpf); sxy = __shfl(sxy, 0, G::lpf); syy = __shfl(syy, 0, G::lpf);
+        sxr = __shfl(sxr, 0, G::lpf); syr = __shfl(syr, 0, G::lpf); chi = __shfl(chi, 0, G::lpf);
+#pragma unroll
+        for (int q = 0; q < G::rounds; ++q) {
+            const int t = sub + q * G::lpf;
+            const double ai = __shfl(jv, ti[q], G::lpf), bi = __shfl(jv, 6 + ti[q], G::lpf);
+            const double aj = __shfl(jv, tj[q], G::lpf), bj = __shfl(jv, 6 + tj[q], G::lpf);
+            if (fv) {
+                if (t < 21) acc[q] += ai * aj * sxx + (ai * bj + bi * aj) * sxy + bi * bj * syy;
+                else if (t < 27) acc[q] += ai * sxr + bi * syr;
+                else if (t == 27) acc[q] += chi;
+            }
         }
         wave_lds_sync();
+    }
+#pragma unroll
+    for (int q = 0; q < G::rounds; ++q) {
+        const int t = sub + q * G::lpf;
+        if (t < 28) part[wave][slotw][t] = acc[q];
+    }
+    __syncthreads();
+    if (threadIdx.x < 28) {  // this workgroup's features, fixed order
+        double s = 0.0;
+        for (int w = 0; w < kFeatWaves; ++w)
+            for (int g = 0; g < G::fpw; ++g) s += part[w][g][threadIdx.x];
+        a.partials[((int64_t)pair * a.chunks + chunk) * 28 + threadIdx.x] = s;
     }
 }
 
 // ------------------------------------------------------------------ K4: normal equations, LM step
 namespace {
-constexpr int kChunks = kSolveThreads / 32;
 struct SolveShared {
-    double part[kChunks][28];
     double tot[28];
     double A[36];
     double tmp[6];
@@ -556,46 +613,16 @@ struct SolveShared {
 };
 }  // namespace
 
-__global__ void __launch_bounds__(kSolveThreads) align_solve_kernel(AlignArgs a, int level) {
+__global__ void __launch_bounds__(64) align_solve_kernel(AlignArgs a, int level) {
     __shared__ SolveShared sh;
     const int pair = blockIdx.x, tid = threadIdx.x;
     PairState& S = a.state[pair];
     const bool last = level == a.min_level;
     if (S.active) {
-        const PairDesc& P = a.pairs[pair];
-        const int nf = P.n_ref + P.n_kf;
-        const int64_t fbase = (int64_t)pair * a.max_f;
-        // thread (term, chunk): 27 terms of J^T W J (lower) / J^T W r plus chi2, 16 feature chunks
-        const int term = tid & 31, chunk = tid >> 5;
-        if (term < 28) {
-            int i = 0, j = 0;
-            if (term < 21) {
-                while ((i + 1) * (i + 2) / 2 <= term) ++i;
-                j = term - i * (i + 1) / 2;
-            } else if (term < 27) {
-                i = term - 21;
-            }
-            double acc = 0.0;
-            for (int f = chunk; f < nf; f += kChunks) {
-                const int64_t gf = fbase + f;
-                if (a.fvis[gf] != 3) continue;
-                const double* fs = a.fsum + 6 * gf;
-                const double* J = a.jimg + 12 * gf;
-                if (term < 21) {
-                    const double ai = J[i], bi = J[6 + i], aj = J[j], bj = J[6 + j];
-                    acc += ai * aj * fs[0] + (ai * bj + bi * aj) * fs[1] + bi * bj * fs[2];
-                } else if (term < 27) {
-                    acc += J[i] * fs[3] + J[6 + i] * fs[4];
-                } else {
-                    acc += fs[5];
-                }
-            }
-            sh.part[chunk][term] = acc;
-        }
-        __syncthreads();
-        if (tid < 28) {
+        if (tid < 28) {  // chunk partials in a fixed order
+            const double* p = a.partials + (int64_t)pair * a.chunks * 28 + tid;
             double s = 0.0;
-            for (int c = 0; c < kChunks; ++c) s += sh.part[c][tid];
+            for (int c = 0; c < a.chunks; ++c) s += p[c * 28];
             sh.tot[tid] = s;
         }
         __syncthreads();
@@ -649,22 +676,17 @@ __global__ void __launch_bounds__(kSolveThreads) align_solve_kernel(AlignArgs a,
 
 // ------------------------------------------------------------------ launch
 template <int kHalf>
-static void launch_level(const AlignArgs& a, int level, hipStream_t s) {
-    using G = Geo<kHalf>;
-    const int fpc = (kFeatThreads / 64) * kFeatPerWave * G::fpw;
-    const int chunks = (a.max_f + fpc - 1) / fpc;
-    hipLaunchKernelGGL(align_residual_kernel<kHalf>, dim3(a.n_pairs * chunks), dim3(kFeatThreads), 0, s, a, level, chunks);
-    hipLaunchKernelGGL(align_scale_kernel, dim3(a.n_pairs), dim3(kSelThreads), 0, s, a, level);
-    hipLaunchKernelGGL(align_weights_kernel<kHalf>, dim3(a.n_pairs * chunks), dim3(kFeatThreads), 0, s, a, level, chunks);
-    hipLaunchKernelGGL(align_solve_kernel, dim3(a.n_pairs), dim3(kSolveThreads), 0, s, a, level);
-}
-
-template <int kHalf>
 static void launch_all(const AlignArgs& a, hipStream_t s) {
     const int64_t nthreads = (int64_t)a.n_pairs * a.max_f;
     const int64_t blocks = (nthreads > a.n_pairs ? nthreads : a.n_pairs) / 256 + 1;
     hipLaunchKernelGGL(align_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
-    for (int level = a.max_level; level >= a.min_level; --level) launch_level<kHalf>(a, level, s);
+    const unsigned fgrid = (unsigned)((int64_t)a.n_pairs * a.chunks);
+    for (int level = a.max_level; level >= a.min_level; --level) {
+        hipLaunchKernelGGL(align_residual_kernel<kHalf>, dim3(fgrid), dim3(kFeatThreads), 0, s, a, level);
+        hipLaunchKernelGGL(align_scale_kernel, dim3(a.n_pairs), dim3(kSelThreads), 0, s, a, level);
+        hipLaunchKernelGGL(align_weights_kernel<kHalf>, dim3(fgrid), dim3(kFeatThreads), 0, s, a, level);
+        hipLaunchKernelGGL(align_solve_kernel, dim3(a.n_pairs), dim3(64), 0, s, a, level);
+    }
 }
 
 void launch_align(const AlignArgs& a, hipStream_t s) {

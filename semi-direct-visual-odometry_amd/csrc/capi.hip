@@ -38,7 +38,7 @@ svo::LevelGeom make_geom(int32_t w, int32_t h, int32_t levels) {
     int64_t off = 0;
     for (int l = 0; l < levels; ++l) {
         g.w[l] = w; g.h[l] = h; g.off[l] = off;
-        off += (int64_t)w * h;
+        off += ((int64_t)w * h + 255) / 256 * 256;  // 256-B aligned level planes (16-B row-block loads)
         w = (w + 1) / 2;
         h = (h + 1) / 2;
     }
@@ -74,7 +74,8 @@ struct svo_align_batch {
     std::vector<uint8_t> pair_set;
     svo::PairDesc* d_pairs;
     svo::PairState* d_state;
-    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_fsum, *d_res, *d_pose_out, *d_err;
+    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_partials, *d_res, *d_pose_out, *d_err;
+    int32_t feat_iters, chunks;
     uint8_t *d_has_point, *d_fvis;
     int32_t* d_status;
     svo_level_trace* d_traces;
@@ -169,7 +170,8 @@ int svo_pyramid_set_create(svo_ctx* c, int32_t n_frames, int32_t width, int32_t 
     p->geom = make_geom(width, height, levels);
     p->grad_off = (p->geom.frame_bytes + 255) / 256 * 256;
     p->stride = (p->grad_off + p->geom.frame_bytes + 255) / 256 * 256;
-    hipError_t e = hipMalloc(&p->d_base, (size_t)p->stride * n_frames);
+    // +64 B: 16-B aligned window-row loads may run up to 31 B past the last plane (zero-weight cells)
+    hipError_t e = hipMalloc(&p->d_base, (size_t)p->stride * n_frames + 64);
     if (e != hipSuccess) {
         delete p;
         return fail(SVO_ERR_HIP, "hipMalloc(pyramids %lld B): %s", (long long)p->stride * n_frames, hipGetErrorString(e));
@@ -236,7 +238,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_jimg,
-                    b->d_state, b->d_fsum, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
+                    b->d_state, b->d_partials, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -272,7 +274,13 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_xw, F * 3 * sizeof(double));
     ALLOC(b->d_jimg, F * 12 * sizeof(double));
     ALLOC(b->d_state, sizeof(svo::PairState) * n_pairs);
-    ALLOC(b->d_fsum, F * 6 * sizeof(double));
+    {
+        const char* env = getenv("SVO_FEAT_ITERS");
+        b->feat_iters = env ? atoi(env) : 4;
+        if (b->feat_iters < 1 || b->feat_iters > 64) b->feat_iters = 4;
+        b->chunks = svo::align_chunks(max_features, half, b->feat_iters);
+    }
+    ALLOC(b->d_partials, (size_t)n_pairs * b->chunks * 28 * sizeof(double));
     ALLOC(b->d_fvis, F);
     b->res_stride = ((int64_t)max_features * area + 2 + 63) / 64 * 64;
     ALLOC(b->d_res, (size_t)n_pairs * b->res_stride * sizeof(double));
@@ -366,7 +374,8 @@ int svo_align_batch_run(svo_align_batch* b) {
     svo::AlignArgs a;
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
-    a.xw = b->d_xw; a.jimg = b->d_jimg; a.state = b->d_state; a.fsum = b->d_fsum; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
+    a.xw = b->d_xw; a.jimg = b->d_jimg; a.state = b->d_state; a.partials = b->d_partials;
+    a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
     a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
     a.min_level = b->params.min_level; a.max_level = b->params.max_level;

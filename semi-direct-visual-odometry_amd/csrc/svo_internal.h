@@ -44,7 +44,7 @@ struct AlignArgs {
     double* xw;               // scratch [n_pairs*max_f][3]   world point per feature
     double* jimg;             // scratch [n_pairs*max_f][12]  image Jacobian at the current level
     uint8_t* fvis;            // scratch [n_pairs*max_f]      bit0 ref visible, bit1 cur visible
-    double* fsum;             // scratch [n_pairs*max_f][6]   S_xx S_xy S_yy S_xr S_yr chi2 per feature
+    double* partials;         // scratch [n_pairs][chunks][28] per-workgroup J^T W J (21) | J^T W r (6) | chi2
     double* res;              // scratch [n_pairs][res_stride] residual per pixel slot (+inf = invisible)
     int64_t res_stride;       // >= max_f*area + 1, even (16-B aligned rows for the 16-B sweeps)
     double* pose_out;         // [n_pairs][7]
@@ -52,12 +52,15 @@ struct AlignArgs {
     int32_t* status_out;      // [n_pairs]
     svo_level_trace* traces;  // [n_pairs][max_level+1]
     int32_t n_pairs, max_f, half, area, min_level, max_level;
+    int32_t feat_iters;       // feature groups one K1/K3 wave walks through
+    int32_t chunks;           // K1/K3 workgroups per pair = align_chunks(max_f, half, feat_iters)
     double fx, fy, cx, cy;
     LevelGeom geom;
 };
 
 void launch_align(const AlignArgs& a, hipStream_t s);
 int align_max_half();  // largest patch half size the alignment kernels are instantiated for
+int align_chunks(int max_f, int half, int feat_iters);  // K1/K3 workgroups per pair
 void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t count, hipStream_t s);
 
 struct FeatureAlignArgs {
