@@ -60,53 +60,70 @@ __device__ __forceinline__ void wave_lds_sync() {  // this wave's LDS writes -> 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// features per K1/K3 workgroup: as many as fit ~40 KB of staged windows, at most 64
+__host__ __device__ constexpr int feats_per_block(int half) {
+    return half <= 3 ? 64 : (half <= 8 ? 32 : 16);
+}
+
 template <int kHalf>
 struct Geo {
     static constexpr int h = kHalf, side = 2 * kHalf + 1, A = side * side;
-    static constexpr int lpf = A <= 16 ? 16 : (A <= 32 ? 32 : 64);  // lanes per feature
-    static constexpr int fpw = 64 / lpf;                               // features per wave
-    static constexpr int RW = 2 * h + 5, CW = 2 * h + 3;               // staged window sides
+    static constexpr int RW = 2 * h + 5, CW = 2 * h + 3;               // staged window sides (ref, cur)
     static constexpr int NB = (RW + 15 + 15) / 16;                     // 16-B blocks per staged row
     static constexpr int pitch = NB * 16;                              // LDS bytes per staged row
-    static constexpr int rbytes = RW * pitch, cbytes = CW * pitch;
-    static constexpr int rounds = (28 + lpf - 1) / lpf;                // normal-equation terms per lane
-    static_assert(RW + CW <= lpf, "one lane per staged row");
+    static constexpr int FPB = feats_per_block(kHalf);                 // features per workgroup
+    static constexpr int fstride1 = (RW + CW) * pitch + 16;            // K1 bytes per feature (ref + cur)
+    static constexpr int fstride3 = RW * pitch + 16;                   // K3 bytes per feature (ref)
+    static constexpr int pix_iters = (FPB * A + kFeatThreads - 1) / kFeatThreads;
 };
 
-// Stage rows [0, ww) of a window with top-left pixel (ox, oy) of an image plane (row pitch W, plane
-// 256-B aligned): lane `row` copies the NB aligned 16-B blocks covering [lin, lin + ww) of its row,
-// lin = (oy + row) * W + ox.  Bytes past the row end are the bytes the reference's unchecked Eigen map
-// would read (they only ever carry a zero bilinear weight).
-template <int ww, int NB>
-__device__ __forceinline__ void stage_rows(uint8_t* dst, const uint8_t* plane, int W, int ox, int oy, int row) {
-    if (row < ww) {
-        const int64_t lin = (int64_t)(oy + row) * W + ox;
-        const uint4* src = reinterpret_cast<const uint4*>(plane + (lin & ~(int64_t)15));
-        uint4* d = reinterpret_cast<uint4*>(dst + row * NB * 16);
-#pragma unroll
-        for (int b = 0; b < NB; ++b) d[b] = src[b];
-    }
-}
-
-// bilinearInterpolationDouble (src/algorithm.cpp:896-905) on a window staged by stage_rows
-template <int NB>
-__device__ __forceinline__ double bilerp_staged(const uint8_t* st, int W, int ox, int oy, double x, double y) {
+// bilinearInterpolationDouble (src/algorithm.cpp:896-905) on a staged window.  Row r of the window
+// (top-left pixel (ox, oy), image row pitch W) holds the aligned 16-B blocks that cover image bytes
+// [lin, lin + width), lin = (oy + r) * W + ox = base + r * W, from byte lin & ~15 on.  Bytes past a row's
+// end are the bytes the reference's unchecked Eigen map would read; they only ever carry a zero weight.
+template <int kPitch>
+__device__ __forceinline__ double bilerp_win(const uint8_t* win, uint32_t base, uint32_t W, int ox, int oy, double x,
+                                             double y) {
     const int32_t x1 = (int32_t)x, y1 = (int32_t)y, x2 = x1 + 1, y2 = y1 + 1;
-    const int64_t lin1 = (int64_t)y1 * W + ox;
-    const uint8_t* r1 = st + (y1 - oy) * NB * 16 + (int)(lin1 & 15) - ox;
-    const uint8_t* r2 = st + (y1 + 1 - oy) * NB * 16 + (int)((lin1 + W) & 15) - ox;
-    const double a = (x2 - x) * r1[x1] + (x - x1) * r1[x2];
-    const double b = (x2 - x) * r2[x1] + (x - x1) * r2[x2];
+    const int ry = y1 - oy, cx = x1 - ox;
+    const uint32_t l1 = base + (uint32_t)ry * W;
+    const uint8_t* r1 = win + ry * kPitch + (int)(l1 & 15u) + cx;
+    const uint8_t* r2 = win + (ry + 1) * kPitch + (int)((l1 + W) & 15u) + cx;
+    const double a = (x2 - x) * r1[0] + (x - x1) * r1[1];
+    const double b = (x2 - x) * r2[0] + (x - x1) * r2[1];
     return (y2 - y) * a + (y - y1) * b;
 }
 
+// copy rows [lin_j, lin_j + width) of an image plane into the LDS window rows, 16-B blocks
+template <int kNB>
+__device__ __forceinline__ void load_row(uint4 (&blk)[kNB], const uint8_t* plane, uint32_t lin) {
+    const uint4* src = reinterpret_cast<const uint4*>(plane + (lin & ~15u));
+#pragma unroll
+    for (int b = 0; b < kNB; ++b) blk[b] = src[b];
+}
+
+// Per-feature records of K1 / K3 (LDS)
+struct ResRec {
+    double ur, vr, cu, cv;     // feature pixel in the ref level, projection into the cur level
+    int32_t rox, roy, cox, coy;  // staged window origins
+    uint32_t rbase, cbase;     // roy * W + rox, coy * W + cox
+    int32_t vis, isref;        // bit0 ref visible, bit1 cur visible; feature of the ref (else the lastKF)
+};
+struct WtRec {
+    double ur, vr;
+    uint32_t rbase;
+    int32_t rox, roy, vis;
+    double ja[6], jb[6];       // computeImageJac at the world point, level-scaled focal lengths
+};
+
 }  // namespace
 
+int align_feat_iters() { return 1; }
+
 int align_chunks(int max_f, int half, int feat_iters) {
-    const int A = (2 * half + 1) * (2 * half + 1);
-    const int fpw = A <= 16 ? 4 : (A <= 32 ? 2 : 1);
-    const int fpc = kFeatWaves * fpw * feat_iters;
-    return (max_f + fpc - 1) / fpc;
+    (void)feat_iters;
+    const int fpb = feats_per_block(half);
+    return (max_f + fpb - 1) / fpb;
 }
 
 // ------------------------------------------------------------------ K0: world points, pair state
@@ -145,83 +162,101 @@ __global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
 }
 
 // ------------------------------------------------------------------ K1: visibility, projection, residuals
-// grid.x = n_pairs * chunks; each wave walks feat_iters feature groups of one pair.
+// grid.x = n_pairs * chunks; a workgroup owns FPB consecutive features of one pair.
+//   1. one lane per feature: border tests, projection, window origins -> LDS record
+//   2. one lane per window row: two aligned 16-B loads per row -> LDS (all rows' loads issued first)
+//   3. one lane per pixel slot (flattened feature x pixel): r = I_cur - T_ref -> contiguous residual row
 template <int kHalf>
 __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs a, int level) {
     using G = Geo<kHalf>;
-    __shared__ __attribute__((aligned(16))) uint8_t win[kFeatWaves][G::fpw][G::rbytes + G::cbytes];
+    constexpr int kRows = G::RW + G::CW;
+    constexpr int kRowIters = (G::FPB * kRows + kFeatThreads - 1) / kFeatThreads;
+    __shared__ __attribute__((aligned(16))) uint8_t win[G::FPB * G::fstride1];
+    __shared__ ResRec rec[G::FPB];
     const int pair = blockIdx.x / a.chunks, chunk = blockIdx.x - pair * a.chunks;
     const PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int sub = lane & (G::lpf - 1), slotw = lane / G::lpf;
+    const int nf = P.n_ref + P.n_kf, f0 = chunk * G::FPB;
+    if (f0 >= nf) return;
+    const int nb = nf - f0 < G::FPB ? nf - f0 : G::FPB;
+    const int tid = threadIdx.x;
     const int W = a.geom.w[level], H = a.geom.h[level];
     const int64_t loff = a.geom.off[level];
-    const double dom = (double)(1 << level), scale = 1.0 / dom;
+    const double scale = 1.0 / (double)(1 << level);
     const int border = G::h + 2;
-    const SE3 pose = se3_load(S.pose);
-    const int64_t fbase = (int64_t)pair * a.max_f;
-    double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
-    uint8_t* wref = win[wave][slotw];
-    uint8_t* wcur = wref + G::rbytes;
-    const int fpc = kFeatWaves * G::fpw * a.feat_iters;  // features per chunk
-    for (int it = 0; it < a.feat_iters; ++it) {
-        const int f0 = chunk * fpc + (it * kFeatWaves + wave) * G::fpw;
-        if (f0 >= nf) break;  // wave-uniform
-        const int f = f0 + slotw;
-        const int64_t gf = fbase + f;
-        uint8_t vis = 0;
-        double ur = 0, vr = 0, cu = 0, cv = 0;
-        if (f < nf && a.has_point[gf]) {
-            ur = a.px[2 * gf] * scale;
-            vr = a.px[2 * gf + 1] * scale;
-            const int ui = (int)floor(ur), vi = (int)floor(vr);
-            if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
-                vis = 1;
-                const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
-                const V3 cp = se3_act(pose, pw);
-                cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
-                cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
-                const int cui = (int)floor(cu), cvi = (int)floor(cv);
-                if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H)) {
-                    vis = 3;
-                    if (sub == 0) {
-                        double ja[6], jb[6];
-                        image_jac(pw, a.fx / dom, a.fy / dom, ja, jb);
-                        for (int j = 0; j < 6; ++j) { a.jimg[12 * gf + j] = ja[j]; a.jimg[12 * gf + 6 + j] = jb[j]; }
+    const int64_t fbase = (int64_t)pair * a.max_f + f0;
+    if (tid < G::FPB) {
+        ResRec R = {};
+        if (tid < nb) {
+            const int64_t gf = fbase + tid;
+            int32_t vis = 0;
+            if (a.has_point[gf]) {
+                const double ur = a.px[2 * gf] * scale, vr = a.px[2 * gf + 1] * scale;
+                const int ui = (int)floor(ur), vi = (int)floor(vr);
+                if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
+                    vis = 1;
+                    const V3 cp = se3_act(se3_load(S.pose), V3{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]});
+                    const double cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
+                    const double cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
+                    const int cui = (int)floor(cu), cvi = (int)floor(cv);
+                    if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H)) {
+                        vis = 3;
+                        R.ur = ur; R.vr = vr; R.cu = cu; R.cv = cv;
+                        R.rox = ui - G::h - 1; R.roy = vi - G::h - 1;
+                        R.cox = cui - G::h; R.coy = cvi - G::h;
+                        R.rbase = (uint32_t)(R.roy * W + R.rox);
+                        R.cbase = (uint32_t)(R.coy * W + R.cox);
                     }
                 }
             }
+            a.fvis[gf] = (uint8_t)vis;
+            R.vis = vis;
+            R.isref = f0 + tid < P.n_ref;
         }
-        if (f < nf && sub == 0) a.fvis[gf] = vis;
-        const int rox = (int)floor(ur) - G::h - 1, roy = (int)floor(vr) - G::h - 1;
-        const int cox = (int)floor(cu) - G::h, coy = (int)floor(cv) - G::h;
-        if (vis == 3) {
-            if (sub < G::RW)
-                stage_rows<G::RW, G::NB>(wref, (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff, W, rox, roy, sub);
-            else
-                stage_rows<G::CW, G::NB>(wcur, P.cur_pyr + loff, W, cox, coy, sub - G::RW);
-        }
-        wave_lds_sync();
-        if (f < nf) {
+        rec[tid] = R;
+    }
+    __syncthreads();
+    uint4 blk[kRowIters][G::NB];
 #pragma unroll
-            for (int k0 = 0; k0 < G::A; k0 += G::lpf) {
-                const int k = k0 + sub;
-                if (k < G::A) {
-                    const int ky = k / G::side - G::h, kx = k % G::side - G::h;
-                    double r = __builtin_inf();
-                    if (vis == 3) {
-                        const double T = bilerp_staged<G::NB>(wref, W, rox, roy, ur + kx, vr + ky);
-                        const double I = bilerp_staged<G::NB>(wcur, W, cox, coy, cu + kx, cv + ky);
-                        r = I - T;
-                    }
-                    res[(int64_t)f * G::A + k] = r;
-                }
-            }
+    for (int i = 0; i < kRowIters; ++i) {
+        const int j = tid + i * kFeatThreads, fl = j / kRows, row = j - fl * kRows;
+        if (fl < nb && rec[fl].vis == 3) {
+            const bool isref = row < G::RW;
+            const uint8_t* plane = (isref ? (rec[fl].isref ? P.ref_pyr : P.kf_pyr) : P.cur_pyr) + loff;
+            load_row<G::NB>(blk[i], plane, isref ? rec[fl].rbase + (uint32_t)(row * W)
+                                                 : rec[fl].cbase + (uint32_t)((row - G::RW) * W));
         }
-        wave_lds_sync();
+    }
+#pragma unroll
+    for (int i = 0; i < kRowIters; ++i) {
+        const int j = tid + i * kFeatThreads, fl = j / kRows, row = j - fl * kRows;
+        if (fl < nb && rec[fl].vis == 3) {
+            uint4* d = reinterpret_cast<uint4*>(win + fl * G::fstride1 + row * G::pitch);
+#pragma unroll
+            for (int b = 0; b < G::NB; ++b) d[b] = blk[i][b];
+        }
+    }
+    __syncthreads();
+    double* __restrict__ res = a.res + (int64_t)pair * a.res_stride + (int64_t)f0 * G::A;
+    const int ne = nb * G::A;
+#pragma unroll 4
+    for (int i = 0; i < G::pix_iters; ++i) {
+        const int e = tid + i * kFeatThreads;
+        if (e < ne) {
+            const int fl = e / G::A, k = e - fl * G::A;
+            const int ky = k / G::side - G::h, kx = k - (k / G::side) * G::side - G::h;
+            const ResRec& R = rec[fl];
+            double r = __builtin_inf();
+            if (R.vis == 3) {
+                const uint8_t* wr = win + fl * G::fstride1;
+                const double T = bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, R.ur + kx, R.vr + ky);
+                const double I = bilerp_win<G::pitch>(wr + G::RW * G::pitch, R.cbase, W, R.cox, R.coy, R.cu + kx,
+                                                      R.cv + ky);
+                r = I - T;
+            }
+            res[e] = r;
+        }
     }
 }
 
@@ -488,118 +523,127 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
 }
 
 // ------------------------------------------------------------------ K3: weights, normal-equation partials
+// Same ownership and phases as K1 (ref windows only).  Per pixel slot: Tukey weight of r, dx/dy from the
+// staged ref window, the Jacobian row J = dx * Jimg0 + dy * Jimg1 (src/image_alignment.cpp:186-188)
+// and its weighted outer product accumulated in registers (21 H terms, 6 g terms, chi2).  A lane's
+// accumulators are then combined by a halving exchange (32 shuffles for 28 terms) and per-wave sums are
+// added in a fixed order: the partials of a workgroup are deterministic.
 template <int kHalf>
 __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a, int level) {
     using G = Geo<kHalf>;
-    __shared__ __attribute__((aligned(16))) uint8_t win[kFeatWaves][G::fpw][G::rbytes];
-    __shared__ double part[kFeatWaves][G::fpw][28];
+    constexpr int kRowIters = (G::FPB * G::RW + kFeatThreads - 1) / kFeatThreads;
+    __shared__ __attribute__((aligned(16))) uint8_t win[G::FPB * G::fstride3];
+    __shared__ WtRec rec[G::FPB];
+    __shared__ double part[kFeatWaves][28];
     const int pair = blockIdx.x / a.chunks, chunk = blockIdx.x - pair * a.chunks;
     const PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int sub = lane & (G::lpf - 1), slotw = lane / G::lpf;
+    const int nf = P.n_ref + P.n_kf, f0 = chunk * G::FPB;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (f0 >= nf) {
+        if (tid < 28) a.partials[((int64_t)pair * a.chunks + chunk) * 28 + tid] = 0.0;
+        return;
+    }
+    const int nb = nf - f0 < G::FPB ? nf - f0 : G::FPB;
     const int W = a.geom.w[level];
     const int64_t loff = a.geom.off[level];
-    const double scale = 1.0 / (double)(1 << level);
+    const double dom = (double)(1 << level), scale = 1.0 / dom;
     const double c = S.c, c2 = c * c;
-    const int64_t fbase = (int64_t)pair * a.max_f;
-    const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
-    uint8_t* wref = win[wave][slotw];
-    // the normal-equation terms this lane owns: t < 21 -> H(i, j) lower, t < 27 -> g(i), t == 27 -> chi2
-    int ti[G::rounds], tj[G::rounds];
-    double acc[G::rounds];
-#pragma unroll
-    for (int q = 0; q < G::rounds; ++q) {
-        const int t = sub + q * G::lpf;
-        int i = 0, j = 0;
-        if (t < 21) {
-            while ((i + 1) * (i + 2) / 2 <= t) ++i;
-            j = t - i * (i + 1) / 2;
-        } else if (t < 27) {
-            i = t - 21;
-        }
-        ti[q] = i;
-        tj[q] = j;
-        acc[q] = 0.0;
-    }
-    const int fpc = kFeatWaves * G::fpw * a.feat_iters;
-    for (int it = 0; it < a.feat_iters; ++it) {
-        const int f0 = chunk * fpc + (it * kFeatWaves + wave) * G::fpw;
-        if (f0 >= nf) break;  // wave-uniform
-        const int f = f0 + slotw;
-        const int64_t gf = fbase + f;
-        const bool fv = f < nf && a.fvis[gf] == 3;
-        double ur = 0, vr = 0, jv = 0.0;
-        int rox = 0, roy = 0;
-        if (fv) {
-            ur = a.px[2 * gf] * scale;
-            vr = a.px[2 * gf + 1] * scale;
-            rox = (int)floor(ur) - G::h - 1;
-            roy = (int)floor(vr) - G::h - 1;
-            stage_rows<G::RW, G::NB>(wref, (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff, W, rox, roy, sub);
-            if (sub < 12) jv = a.jimg[12 * gf + sub];
-        }
-        wave_lds_sync();
-        double sxx = 0, sxy = 0, syy = 0, sxr = 0, syr = 0, chi = 0;
-        if (fv) {
-#pragma unroll
-            for (int k0 = 0; k0 < G::A; k0 += G::lpf) {
-                const int k = k0 + sub;
-                if (k < G::A) {
-                    const int ky = k / G::side - G::h, kx = k % G::side - G::h;
-                    const double r = res[(int64_t)f * G::A + k];
-                    double w = 0.0;
-                    if (fabs(r) <= c) {
-                        const double t = 1.0 - (r * r) / c2;
-                        w = t * t;
-                    }
-                    chi += r * r * w;
-                    if (w != 0.0) {
-                        const double row = vr + ky, col = ur + kx;
-                        const double dx = 0.5 * (bilerp_staged<G::NB>(wref, W, rox, roy, col + 1, row) -
-                                                 bilerp_staged<G::NB>(wref, W, rox, roy, col - 1, row));
-                        const double dy = 0.5 * (bilerp_staged<G::NB>(wref, W, rox, roy, col, row + 1) -
-                                                 bilerp_staged<G::NB>(wref, W, rox, roy, col, row - 1));
-                        const double wdx = w * dx, wdy = w * dy;
-                        sxx += wdx * dx; sxy += wdx * dy; syy += wdy * dy; sxr += wdx * r; syr += wdy * r;
-                    }
-                }
+    const int64_t fbase = (int64_t)pair * a.max_f + f0;
+    const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride + (int64_t)f0 * G::A;
+    const int ne = nb * G::A;
+    if (tid < G::FPB) {
+        WtRec R = {};
+        if (tid < nb) {
+            const int64_t gf = fbase + tid;
+            if (a.fvis[gf] == 3) {
+                R.vis = 3;
+                R.ur = a.px[2 * gf] * scale;
+                R.vr = a.px[2 * gf + 1] * scale;
+                R.rox = (int)floor(R.ur) - G::h - 1;
+                R.roy = (int)floor(R.vr) - G::h - 1;
+                R.rbase = (uint32_t)(R.roy * W + R.rox);
+                image_jac(V3{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]}, a.fx / dom, a.fy / dom, R.ja, R.jb);
             }
         }
-#pragma unroll
-        for (int o = G::lpf >> 1; o > 0; o >>= 1) {
-            sxx += __shfl_down(sxx, o, G::lpf); sxy += __shfl_down(sxy, o, G::lpf); syy += __shfl_down(syy, o, G::lpf);
-            sxr += __shfl_down(sxr, o, G::lpf); syr += __shfl_down(syr, o, G::lpf); chi += __shfl_down(chi, o, G::lpf);
-        }
-        // every lane of the group gets the feature's sums and the Jimg entries of its terms
-        sxx = __shfl(sxx, 0, G::lpf); sxy = __shfl(sxy, 0, G::lpf); syy = __shfl(syy, 0, G::lpf);
-        sxr = __shfl(sxr, 0, G::lpf); syr = __shfl(syr, 0, G::lpf); chi = __shfl(chi, 0, G::lpf);
-#pragma unroll
-        for (int q = 0; q < G::rounds; ++q) {
-            const int t = sub + q * G::lpf;
-            const double ai = __shfl(jv, ti[q], G::lpf), bi = __shfl(jv, 6 + ti[q], G::lpf);
-            const double aj = __shfl(jv, tj[q], G::lpf), bj = __shfl(jv, 6 + tj[q], G::lpf);
-            if (fv) {
-                if (t < 21) acc[q] += ai * aj * sxx + (ai * bj + bi * aj) * sxy + bi * bj * syy;
-                else if (t < 27) acc[q] += ai * sxr + bi * syr;
-                else if (t == 27) acc[q] += chi;
-            }
-        }
-        wave_lds_sync();
-    }
-#pragma unroll
-    for (int q = 0; q < G::rounds; ++q) {
-        const int t = sub + q * G::lpf;
-        if (t < 28) part[wave][slotw][t] = acc[q];
+        rec[tid] = R;
     }
     __syncthreads();
-    if (threadIdx.x < 28) {  // this workgroup's features, fixed order
+    {
+        uint4 blk[kRowIters][G::NB];
+#pragma unroll
+        for (int i = 0; i < kRowIters; ++i) {
+            const int j = tid + i * kFeatThreads, fl = j / G::RW, row = j - fl * G::RW;
+            if (fl < nb && rec[fl].vis == 3)
+                load_row<G::NB>(blk[i], (f0 + fl < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff,
+                                rec[fl].rbase + (uint32_t)(row * W));
+        }
+#pragma unroll
+        for (int i = 0; i < kRowIters; ++i) {
+            const int j = tid + i * kFeatThreads, fl = j / G::RW, row = j - fl * G::RW;
+            if (fl < nb && rec[fl].vis == 3) {
+                uint4* d = reinterpret_cast<uint4*>(win + fl * G::fstride3 + row * G::pitch);
+#pragma unroll
+                for (int b = 0; b < G::NB; ++b) d[b] = blk[i][b];
+            }
+        }
+    }
+    __syncthreads();
+    double acc[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) acc[t] = 0.0;
+#pragma unroll 2
+    for (int i = 0; i < G::pix_iters; ++i) {
+        const int e = tid + i * kFeatThreads;
+        if (e >= ne) break;
+        const int fl = e / G::A, k = e - fl * G::A;
+        const WtRec& R = rec[fl];
+        if (R.vis != 3) continue;
+        const double r = res[e];
+        if (!(fabs(r) <= c)) continue;  // w = 0: no H, g or chi2 contribution (src/optimizer.cpp:502-511)
+        const double tt = 1.0 - (r * r) / c2;
+        const double w = tt * tt;
+        acc[27] += r * r * w;
+        const int ky = k / G::side - G::h, kx = k - (k / G::side) * G::side - G::h;
+        const double row = R.vr + ky, col = R.ur + kx;
+        const uint8_t* wr = win + fl * G::fstride3;
+        const double dx = 0.5 * (bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col + 1, row) -
+                                 bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col - 1, row));
+        const double dy = 0.5 * (bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col, row + 1) -
+                                 bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col, row - 1));
+        double J[6], wJ[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            J[q] = dx * R.ja[q] + dy * R.jb[q];
+            wJ[q] = w * J[q];
+        }
+        int t = 0;
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+#pragma unroll
+            for (int p = 0; p <= q; ++p) acc[t++] += wJ[q] * J[p];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) acc[21 + q] += wJ[q] * r;
+    }
+    // halving exchange: after the steps of offsets 32..2 lane L holds term L >> 1 (half of it)
+#pragma unroll
+    for (int o = 32, n = 32; o >= 2; o >>= 1, n >>= 1) {
+        const bool up = (lane & o) != 0;
+#pragma unroll
+        for (int q = 0; q < n / 2; ++q) {
+            const double keep = up ? acc[q + n / 2] : acc[q];
+            const double send = up ? acc[q] : acc[q + n / 2];
+            acc[q] = keep + __shfl_xor(send, o, 64);
+        }
+    }
+    acc[0] += __shfl_xor(acc[0], 1, 64);
+    if ((lane & 1) == 0 && (lane >> 1) < 28) part[wave][lane >> 1] = acc[0];
+    __syncthreads();
+    if (tid < 28) {
         double s = 0.0;
-        for (int w = 0; w < kFeatWaves; ++w)
-            for (int g = 0; g < G::fpw; ++g) s += part[w][g][threadIdx.x];
-        a.partials[((int64_t)pair * a.chunks + chunk) * 28 + threadIdx.x] = s;
+        for (int w = 0; w < kFeatWaves; ++w) s += part[w][tid];
+        a.partials[((int64_t)pair * a.chunks + chunk) * 28 + tid] = s;
     }
 }
 

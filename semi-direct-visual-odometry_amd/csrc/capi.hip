@@ -275,9 +275,7 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_jimg, F * 12 * sizeof(double));
     ALLOC(b->d_state, sizeof(svo::PairState) * n_pairs);
     {
-        const char* env = getenv("SVO_FEAT_ITERS");
-        b->feat_iters = env ? atoi(env) : 4;
-        if (b->feat_iters < 1 || b->feat_iters > 64) b->feat_iters = 4;
+        b->feat_iters = svo::align_feat_iters();
         b->chunks = svo::align_chunks(max_features, half, b->feat_iters);
     }
     ALLOC(b->d_partials, (size_t)n_pairs * b->chunks * 28 * sizeof(double));

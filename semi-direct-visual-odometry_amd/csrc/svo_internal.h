@@ -60,6 +60,7 @@ struct AlignArgs {
 
 void launch_align(const AlignArgs& a, hipStream_t s);
 int align_max_half();  // largest patch half size the alignment kernels are instantiated for
+int align_feat_iters();                                 // feature groups per K1/K3 wave
 int align_chunks(int max_f, int half, int feat_iters);  // K1/K3 workgroups per pair
 void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t count, hipStream_t s);
 
