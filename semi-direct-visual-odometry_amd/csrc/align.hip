@@ -94,12 +94,16 @@ __device__ __forceinline__ double bilerp_win(const uint8_t* win, uint32_t base, 
     return (y2 - y) * a + (y - y1) * b;
 }
 
-// copy rows [lin_j, lin_j + width) of an image plane into the LDS window rows, 16-B blocks
-template <int kNB>
-__device__ __forceinline__ void load_row(uint4 (&blk)[kNB], const uint8_t* plane, uint32_t lin) {
-    const uint4* src = reinterpret_cast<const uint4*>(plane + (lin & ~15u));
-#pragma unroll
-    for (int b = 0; b < kNB; ++b) blk[b] = src[b];
+// 16-B load from an image plane.  The plane pointers come from the device-resident pair table, so the
+// compiler only sees generic pointers; the explicit global address space keeps these loads off the flat
+// path (a flat load also waits on LDS traffic, which serialises the staging loop).
+__device__ __forceinline__ uint4 gload16(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(1))) const uint4 gu4;
+    return *(gu4*)(p);
+#else
+    return *reinterpret_cast<const uint4*>(p);  // host pass only parses device code
+#endif
 }
 
 // Per-feature records of K1 / K3 (LDS)
@@ -186,11 +190,14 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
     const double scale = 1.0 / (double)(1 << level);
     const int border = G::h + 2;
     const int64_t fbase = (int64_t)pair * a.max_f + f0;
+    const uint8_t* const ref_plane = P.ref_pyr + loff;
+    const uint8_t* const kf_plane = P.kf_pyr + loff;
+    const uint8_t* const cur_plane = P.cur_pyr + loff;
     if (tid < G::FPB) {
-        ResRec R = {};
+        ResRec& R = rec[tid];
+        int32_t vis = 0;
         if (tid < nb) {
             const int64_t gf = fbase + tid;
-            int32_t vis = 0;
             if (a.has_point[gf]) {
                 const double ur = a.px[2 * gf] * scale, vr = a.px[2 * gf + 1] * scale;
                 const int ui = (int)floor(ur), vi = (int)floor(vr);
@@ -205,33 +212,36 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
                         R.ur = ur; R.vr = vr; R.cu = cu; R.cv = cv;
                         R.rox = ui - G::h - 1; R.roy = vi - G::h - 1;
                         R.cox = cui - G::h; R.coy = cvi - G::h;
-                        R.rbase = (uint32_t)(R.roy * W + R.rox);
-                        R.cbase = (uint32_t)(R.coy * W + R.cox);
+                        R.rbase = (uint32_t)((vi - G::h - 1) * W + ui - G::h - 1);
+                        R.cbase = (uint32_t)((cvi - G::h) * W + cui - G::h);
                     }
                 }
             }
             a.fvis[gf] = (uint8_t)vis;
-            R.vis = vis;
             R.isref = f0 + tid < P.n_ref;
         }
-        rec[tid] = R;
+        R.vis = vis;
     }
     __syncthreads();
+    // every row's loads first (branch-free: rows of features without a window read a harmless in-plane
+    // block), then the LDS stores
     uint4 blk[kRowIters][G::NB];
 #pragma unroll
     for (int i = 0; i < kRowIters; ++i) {
-        const int j = tid + i * kFeatThreads, fl = j / kRows, row = j - fl * kRows;
-        if (fl < nb && rec[fl].vis == 3) {
-            const bool isref = row < G::RW;
-            const uint8_t* plane = (isref ? (rec[fl].isref ? P.ref_pyr : P.kf_pyr) : P.cur_pyr) + loff;
-            load_row<G::NB>(blk[i], plane, isref ? rec[fl].rbase + (uint32_t)(row * W)
-                                                 : rec[fl].cbase + (uint32_t)((row - G::RW) * W));
-        }
+        const int j = tid + i * kFeatThreads;
+        const int fl = j / kRows < G::FPB ? j / kRows : G::FPB - 1, row = j - fl * kRows;
+        const bool ok = rec[fl].vis == 3, isref = row < G::RW;
+        const uint8_t* plane = isref ? (rec[fl].isref ? ref_plane : kf_plane) : cur_plane;
+        const uint32_t lin = !ok ? 0u : (isref ? rec[fl].rbase + (uint32_t)(row * W)
+                                              : rec[fl].cbase + (uint32_t)((row - G::RW) * W));
+        const uint8_t* src = plane + (lin & ~15u);
+#pragma unroll
+        for (int b = 0; b < G::NB; ++b) blk[i][b] = gload16(src + 16 * b);
     }
 #pragma unroll
     for (int i = 0; i < kRowIters; ++i) {
         const int j = tid + i * kFeatThreads, fl = j / kRows, row = j - fl * kRows;
-        if (fl < nb && rec[fl].vis == 3) {
+        if (j < G::FPB * kRows) {
             uint4* d = reinterpret_cast<uint4*>(win + fl * G::fstride1 + row * G::pitch);
 #pragma unroll
             for (int b = 0; b < G::NB; ++b) d[b] = blk[i][b];
@@ -553,55 +563,61 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
     const int64_t fbase = (int64_t)pair * a.max_f + f0;
     const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride + (int64_t)f0 * G::A;
     const int ne = nb * G::A;
+    const uint8_t* const ref_plane = P.ref_pyr + loff;
+    const uint8_t* const kf_plane = P.kf_pyr + loff;
+    // the first kPre residuals of this lane, loaded before the setup so their latency overlaps it
+    constexpr int kPre = G::pix_iters < 8 ? G::pix_iters : 8;
+    double rr[kPre];
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+        const int e = tid + i * kFeatThreads;
+        rr[i] = e < ne ? res[e] : 0.0;
+    }
     if (tid < G::FPB) {
-        WtRec R = {};
+        WtRec& R = rec[tid];
+        int32_t vis = 0;
         if (tid < nb) {
             const int64_t gf = fbase + tid;
             if (a.fvis[gf] == 3) {
-                R.vis = 3;
-                R.ur = a.px[2 * gf] * scale;
-                R.vr = a.px[2 * gf + 1] * scale;
-                R.rox = (int)floor(R.ur) - G::h - 1;
-                R.roy = (int)floor(R.vr) - G::h - 1;
-                R.rbase = (uint32_t)(R.roy * W + R.rox);
+                vis = 3;
+                const double ur = a.px[2 * gf] * scale, vr = a.px[2 * gf + 1] * scale;
+                const int rox = (int)floor(ur) - G::h - 1, roy = (int)floor(vr) - G::h - 1;
+                R.ur = ur; R.vr = vr; R.rox = rox; R.roy = roy;
+                R.rbase = (uint32_t)(roy * W + rox);
                 image_jac(V3{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]}, a.fx / dom, a.fy / dom, R.ja, R.jb);
             }
         }
-        rec[tid] = R;
+        R.vis = vis;
     }
     __syncthreads();
-    {
-        uint4 blk[kRowIters][G::NB];
+    uint4 blk[kRowIters][G::NB];  // all loads first, then the LDS stores (see K1)
 #pragma unroll
-        for (int i = 0; i < kRowIters; ++i) {
-            const int j = tid + i * kFeatThreads, fl = j / G::RW, row = j - fl * G::RW;
-            if (fl < nb && rec[fl].vis == 3)
-                load_row<G::NB>(blk[i], (f0 + fl < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff,
-                                rec[fl].rbase + (uint32_t)(row * W));
-        }
+    for (int i = 0; i < kRowIters; ++i) {
+        const int j = tid + i * kFeatThreads;
+        const int fl = j / G::RW < G::FPB ? j / G::RW : G::FPB - 1, row = j - fl * G::RW;
+        const uint8_t* plane = f0 + fl < P.n_ref ? ref_plane : kf_plane;
+        const uint32_t lin = rec[fl].vis == 3 ? rec[fl].rbase + (uint32_t)(row * W) : 0u;
+        const uint8_t* src = plane + (lin & ~15u);
 #pragma unroll
-        for (int i = 0; i < kRowIters; ++i) {
-            const int j = tid + i * kFeatThreads, fl = j / G::RW, row = j - fl * G::RW;
-            if (fl < nb && rec[fl].vis == 3) {
-                uint4* d = reinterpret_cast<uint4*>(win + fl * G::fstride3 + row * G::pitch);
+        for (int b = 0; b < G::NB; ++b) blk[i][b] = gload16(src + 16 * b);
+    }
 #pragma unroll
-                for (int b = 0; b < G::NB; ++b) d[b] = blk[i][b];
-            }
+    for (int i = 0; i < kRowIters; ++i) {
+        const int j = tid + i * kFeatThreads, fl = j / G::RW, row = j - fl * G::RW;
+        if (j < G::FPB * G::RW) {
+            uint4* d = reinterpret_cast<uint4*>(win + fl * G::fstride3 + row * G::pitch);
+#pragma unroll
+            for (int b = 0; b < G::NB; ++b) d[b] = blk[i][b];
         }
     }
     __syncthreads();
     double acc[32];
 #pragma unroll
     for (int t = 0; t < 32; ++t) acc[t] = 0.0;
-#pragma unroll 2
-    for (int i = 0; i < G::pix_iters; ++i) {
-        const int e = tid + i * kFeatThreads;
-        if (e >= ne) break;
+    auto pixel = [&](int e, double r) {
         const int fl = e / G::A, k = e - fl * G::A;
         const WtRec& R = rec[fl];
-        if (R.vis != 3) continue;
-        const double r = res[e];
-        if (!(fabs(r) <= c)) continue;  // w = 0: no H, g or chi2 contribution (src/optimizer.cpp:502-511)
+        if (R.vis != 3 || !(fabs(r) <= c)) return;  // w = 0: no H, g or chi2 term (src/optimizer.cpp:502-511)
         const double tt = 1.0 - (r * r) / c2;
         const double w = tt * tt;
         acc[27] += r * r * w;
@@ -625,6 +641,15 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
             for (int p = 0; p <= q; ++p) acc[t++] += wJ[q] * J[p];
 #pragma unroll
         for (int q = 0; q < 6; ++q) acc[21 + q] += wJ[q] * r;
+    };
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+        const int e = tid + i * kFeatThreads;
+        if (e < ne) pixel(e, rr[i]);
+    }
+    for (int i = kPre; i < G::pix_iters; ++i) {
+        const int e = tid + i * kFeatThreads;
+        if (e < ne) pixel(e, res[e]);
     }
     // halving exchange: after the steps of offsets 32..2 lane L holds term L >> 1 (half of it)
 #pragma unroll
