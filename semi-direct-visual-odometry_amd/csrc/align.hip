@@ -32,12 +32,14 @@ namespace {
 
 constexpr int kFeatThreads = 256;    // K1 / K3 workgroup (4 waves)
 constexpr int kFeatWaves = kFeatThreads / 64;
-constexpr int kSelThreads = 1024;    // K2 workgroup
+constexpr int kSelThreads = 512;     // K2 workgroup (two per CU)
 constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kBins = 4096;
 constexpr double kBinScale = 32.0;   // bins per grey level
 constexpr double kBinOffset = 64.0;  // signed map covers [-64, 64); outliers clamp to the end bins
-constexpr int kCandCap = 4096;
+constexpr double kKeyScale = 512.0;  // K1's 16-bit residual key: 16 keys per value bin
+constexpr uint32_t kKeyMax = 65534;  // largest key of a visible slot; 0xFFFF = invisible
+constexpr int kCandCap = 2048;
 constexpr int kRankCap = 256;        // <= this many candidates: rank counting, else bitonic sort
 constexpr int kRadixBits = 11;
 constexpr double kDblMax = 1.7976931348623157e308;
@@ -49,6 +51,14 @@ __device__ __forceinline__ double wave_sum(double v) {
 __device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
     return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_down(v, o, 64));
+    return __shfl(v, 0, 64);
+}
+__device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_down(v, o, 64));
+    return __shfl(v, 0, 64);
 }
 __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
@@ -106,6 +116,14 @@ __device__ __forceinline__ uint4 gload16(const uint8_t* p) {
 #endif
 }
 
+// 16-bit monotone key of a residual for K2's sweeps: floor((r + 64) * 512) clamped to [0, kKeyMax];
+// 0xFFFF marks an invisible slot.  key >> 4 is exactly the value bin floor((r + 64) * 32) of K2.
+__device__ __forceinline__ uint16_t res_key(double r) {
+    if (r == __builtin_inf()) return 0xFFFF;
+    const double t = (r + kBinOffset) * kKeyScale;
+    return (uint16_t)(t < 0.0 ? 0u : (t >= (double)kKeyMax ? kKeyMax : (uint32_t)t));
+}
+
 // Per-feature records of K1 / K3 (LDS)
 struct ResRec {
     double ur, vr, cu, cv;     // feature pixel in the ref level, projection into the cur level
@@ -143,6 +161,7 @@ __global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
         S.status = P.n_ref == 0 ? kFailed : kNonSuffPoints;
         const int64_t M = (int64_t)nf * a.area;
         if (M & 1) a.res[gid * a.res_stride + M] = __builtin_inf();  // pad for the 16-B sweeps of K2
+        for (int64_t s = M; s < ((M + 7) & ~(int64_t)7); ++s) a.keys[gid * a.key_stride + s] = 0xFFFF;
         svo_level_trace* tr = a.traces + gid * (a.max_level + 1);
         for (int l = 0; l <= a.max_level; ++l) {
             svo_level_trace t = {};
@@ -249,6 +268,7 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
     }
     __syncthreads();
     double* __restrict__ res = a.res + (int64_t)pair * a.res_stride + (int64_t)f0 * G::A;
+    uint16_t* __restrict__ keys = a.keys + (int64_t)pair * a.key_stride + (int64_t)f0 * G::A;
     const int ne = nb * G::A;
 #pragma unroll 4
     for (int i = 0; i < G::pix_iters; ++i) {
@@ -266,6 +286,7 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
                 r = I - T;
             }
             res[e] = r;
+            keys[e] = res_key(r);
         }
     }
 }
@@ -274,13 +295,18 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
 namespace {
 
 struct SelShared {
-    uint32_t hist[kBins];
+    uint32_t hist[kBins];   // value bins of r (median), radix digits (exact fallback)
+    uint32_t hlo[kBins];    // MAD bracket: bins of the lower / upper bound of |r - med| per value bin
+    uint32_t hhi[kBins];    // (hhi is reused by cand_select's fine histogram)
     double cand[kCandCap];
+    uint32_t mcand[kCandCap];  // MAD candidate slots
+    double small[kRankCap];    // values of one fine bin (cand_select)
     uint32_t scan[kSelWaves];
     uint32_t ired[kSelWaves][2];
-    double red[kSelWaves];
+    double red[kSelWaves], red2[kSelWaves];
     uint64_t sel_prefix;
-    uint32_t sel_k, sel_cnt, sel_bits, sel_bin, cand_n;
+    uint32_t sel_k, sel_cnt, sel_bits, sel_bin, cand_n, mcand_n, small_n;
+    uint32_t rngw[kSelWaves][4];
     double sel_hi, sel_lo;
 };
 
@@ -310,6 +336,42 @@ __device__ __forceinline__ void sweep_res(const double* __restrict__ res, int M,
             if (v[u].y != __builtin_inf()) fn(v[u].y);
         }
     }
+}
+
+// Sweep the 16-bit residual keys of K1; fn(slot, key) for each visible slot.  A lane owns kKeyLoads
+// 16-B groups of 8 keys per chunk and issues all of a chunk's loads before using any (one memory round
+// trip per chunk; a config-2 pair, 50 000 slots, is one chunk).  Rows are padded with 0xFFFF to 8.
+constexpr int kKeyLoads = 13;
+template <typename Fn>
+__device__ __forceinline__ void sweep_keys(const uint16_t* __restrict__ keys, int M8, Fn fn) {
+    const int tid = threadIdx.x;
+    for (int base = 8 * tid; base < M8; base += 8 * kSelThreads * kKeyLoads) {
+        uint4 v[kKeyLoads];
+#pragma unroll
+        for (int u = 0; u < kKeyLoads; ++u) {
+            const int s = base + u * 8 * kSelThreads;
+            v[u] = s < M8 ? *reinterpret_cast<const uint4*>(keys + s) : make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kKeyLoads; ++u) {
+            const int s = base + u * 8 * kSelThreads;
+            const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((w[q] & 0xFFFFu) != 0xFFFFu) fn(s + 2 * q, w[q] & 0xFFFFu);
+                if ((w[q] >> 16) != 0xFFFFu) fn(s + 2 * q + 1, w[q] >> 16);
+            }
+        }
+    }
+}
+
+// distance bounds between the values of value bin j and a median known to lie in [mlo, mhi]
+__device__ __forceinline__ void bin_dist(int j, double mlo, double mhi, double& dlo, double& dhi) {
+    constexpr double eps = 1e-9;  // r + kBinOffset rounds by < 2^-45 before binning
+    const double lo = j == 0 ? -__builtin_inf() : (double)j / kBinScale - kBinOffset - eps;
+    const double hi = j == kBins - 1 ? __builtin_inf() : (double)(j + 1) / kBinScale - kBinOffset + eps;
+    dlo = fmax(0.0, fmax(lo - mhi, mlo - hi));
+    dhi = fmax(hi - mlo, mhi - lo);
 }
 
 // bin holding rank sh.sel_k of hist -> sh.sel_bin, sh.sel_k (rank inside the bin), sh.sel_cnt
@@ -350,15 +412,16 @@ __device__ void find_bin(SelShared& sh, const uint32_t* hist, int bins) {
     __syncthreads();
 }
 
-// k-th and (k-1)-th smallest of cand[0..n) (k-1 only if want_lo and k > 0)
-__device__ void cand_select(SelShared& sh, uint32_t n, uint32_t kk, bool want_lo) {
+// k-th and (k-1)-th smallest of v[0..n) (k-1 only if want_lo and k > 0): rank counting for small n,
+// else a bitonic sort (v must then be sh.cand)
+__device__ void select_direct(SelShared& sh, double* v, uint32_t n, uint32_t kk, bool want_lo) {
     const int tid = threadIdx.x;
     if (n <= (uint32_t)kRankCap) {
         for (uint32_t i = tid; i < n; i += kSelThreads) {
-            const double vi = sh.cand[i];
+            const double vi = v[i];
             uint32_t rank = 0;
             for (uint32_t j = 0; j < n; ++j) {
-                const double vj = sh.cand[j];
+                const double vj = v[j];
                 rank += (vj < vi) | ((vj == vi) & (j < i));
             }
             if (rank == kk) sh.sel_hi = vi;
@@ -385,6 +448,71 @@ __device__ void cand_select(SelShared& sh, uint32_t n, uint32_t kk, bool want_lo
         sh.sel_hi = sh.cand[kk];
         if (want_lo && kk > 0) sh.sel_lo = sh.cand[kk - 1];
     }
+    __syncthreads();
+}
+
+// append for the lanes with pred set: one LDS atomic per wave, slots in lane order
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+    const uint64_t m = __ballot(pred);
+    const int lane = threadIdx.x & 63;
+    if (m == 0) return 0;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// k-th (and (k-1)-th) smallest of sh.cand[0..n).  Above kRankCap values, a 2048-bin histogram over
+// the candidates' range narrows to one bin whose values are ranked directly (bitonic sort if that bin
+// is still large).
+__device__ void cand_select(SelShared& sh, uint32_t n, uint32_t kk, bool want_lo) {
+    if (n <= (uint32_t)kRankCap) {
+        select_direct(sh, sh.cand, n, kk, want_lo);
+        return;
+    }
+    constexpr int kFine = 2048;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double vmin = __builtin_inf(), vmax = -__builtin_inf();
+    for (uint32_t i = tid; i < n; i += kSelThreads) { vmin = fmin(vmin, sh.cand[i]); vmax = fmax(vmax, sh.cand[i]); }
+    vmin = -wave_max(-vmin);
+    vmax = wave_max(vmax);
+    if (lane == 0) { sh.red[wave] = vmax; sh.red2[wave] = vmin; }
+    for (int i = tid; i < kFine; i += kSelThreads) sh.hhi[i] = 0;
+    if (tid == 0) sh.small_n = 0;
+    __syncthreads();
+    vmin = __builtin_inf(); vmax = -__builtin_inf();
+    for (int w = 0; w < kSelWaves; ++w) { vmax = fmax(vmax, sh.red[w]); vmin = fmin(vmin, sh.red2[w]); }
+    if (!(vmax > vmin) || !(vmax - vmin < __builtin_inf())) {
+        select_direct(sh, sh.cand, n, kk, want_lo);
+        return;
+    }
+    const double inv = (double)kFine / (vmax - vmin);
+    auto fbin = [=](double v) { const int b = (int)((v - vmin) * inv); return b < kFine - 1 ? b : kFine - 1; };
+    for (uint32_t i = tid; i < n; i += kSelThreads) atomicAdd(&sh.hhi[fbin(sh.cand[i])], 1u);
+    if (tid == 0) sh.sel_k = kk;
+    __syncthreads();
+    find_bin(sh, sh.hhi, kFine);
+    const uint32_t b2 = sh.sel_bin, kin = sh.sel_k, c2 = sh.sel_cnt;
+    if (c2 > (uint32_t)kRankCap) {
+        select_direct(sh, sh.cand, n, kk, want_lo);
+        return;
+    }
+    double below_max = -__builtin_inf();
+    for (uint32_t i = tid; i < n; i += kSelThreads) {
+        const double v = sh.cand[i];
+        const int b = fbin(v);
+        const uint32_t s = wave_append(&sh.small_n, b == (int)b2);
+        if (b == (int)b2) sh.small[s] = v;
+        else if (b < (int)b2) below_max = fmax(below_max, v);
+    }
+    below_max = wave_max(below_max);
+    if (lane == 0) sh.red[wave] = below_max;
+    __syncthreads();
+    below_max = -__builtin_inf();
+    for (int w = 0; w < kSelWaves; ++w) below_max = fmax(below_max, sh.red[w]);
+    select_direct(sh, sh.small, c2, kin, want_lo && kin > 0);
+    if (want_lo && kin == 0 && tid == 0) sh.sel_lo = below_max;
     __syncthreads();
 }
 
@@ -482,23 +610,49 @@ __device__ double block_median(SelShared& sh, const double* __restrict__ res, in
 
 }  // namespace
 
+#if defined(SVO_STAMPS)
+// diagnostic build only (make stamps): per (pair, level) cycle stamps of K2's phases
+__device__ uint64_t g_stamps[4096 * 16];
+#define K2_STAMP(i, v)                                                                      \
+    do {                                                                                    \
+        if (tid == 0 && pair * 5 + level < 4096) g_stamps[(pair * 5 + level) * 16 + (i)] = (v); \
+    } while (0)
+#else
+#define K2_STAMP(i, v) \
+    do {               \
+    } while (0)
+#endif
+
+// One workgroup per pair (src/algorithm.cpp:834-872 on the level's residual vector).
+//   1. value-bin histogram of the visible residuals from K1's 16-bit keys (key >> 4 = value bin);
+//      the bin b holding rank n/2 and its count
+//   2. MAD bracket without touching the slots again: every value bin j bounds |r - med| of its members
+//      (med lies in bin b, or is exact on the slow path); the order statistic n/2 of those lower and
+//      upper bounds brackets the MAD in [L0, U0).  Bins wholly below L0 are counted, bins meeting
+//      [L0, U0) are MAD candidates, the rest lie above
+//   3. one sweep over the keys gathers the slots of bin b (median candidates) and of the candidate
+//      bins; only those slots' exact residuals are read
+//   4. exact selection among the candidates (rank counting or bitonic sort in LDS)
+// Cases the fast path cannot settle (overfull bins; the even-length neighbour below a bin's first
+// element) take the exact path on the 8-B residuals.
 __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, int level) {
     __shared__ SelShared sh;
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf, M = nf * a.area;
+    const int nf = P.n_ref + P.n_kf, M = nf * a.area, M8 = (M + 7) & ~7;
     const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
+    const uint16_t* __restrict__ keys = a.keys + (int64_t)pair * a.key_stride;
     const uint8_t* __restrict__ fvis = a.fvis + (int64_t)pair * a.max_f;
-    // visible features (Frame border tests of K1) and the median histogram
+    K2_STAMP(0, clock64());
     uint32_t nrv = 0, ncv = 0;
     for (int f = tid; f < nf; f += kSelThreads) {
         const uint8_t v = fvis[f];
         nrv += v & 1;
         ncv += v >> 1;
     }
-    for (int i = tid; i < kBins; i += kSelThreads) sh.hist[i] = 0;
+    for (int i = tid; i < kBins; i += kSelThreads) { sh.hist[i] = 0; sh.hlo[i] = 0; sh.hhi[i] = 0; }
     nrv = wave_sum_u(nrv);
     ncv = wave_sum_u(ncv);
     if (lane == 0) { sh.ired[wave][0] = nrv; sh.ired[wave][1] = ncv; }
@@ -506,19 +660,126 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
     nrv = 0; ncv = 0;
     for (int w = 0; w < kSelWaves; ++w) { nrv += sh.ired[w][0]; ncv += sh.ired[w][1]; }
     const uint32_t n = ncv * (uint32_t)a.area;
-    sweep_res(res, M, [&](double r) { atomicAdd(&sh.hist[sel_bin<false>(r)], 1u); });
-    __syncthreads();
-    double med, mad;
-    if (n == 0) {
-        med = kDblMax;  // every slot is DBL_MAX in the reference
-        mad = 0.0;
-    } else {
-        med = block_median<false>(sh, res, M, n, 0.0);
-        for (int i = tid; i < kBins; i += kSelThreads) sh.hist[i] = 0;
+    const uint32_t mid = n / 2;
+    const bool want_lo = ((M & 1) == 0) && mid > 0;
+    double med = kDblMax, mad = 0.0;  // n == 0: every slot is DBL_MAX in the reference
+    if (n > 0) {
+        K2_STAMP(1, clock64());
+        sweep_keys(keys, M8, [&](int, uint32_t q) { atomicAdd(&sh.hist[q >> 4], 1u); });
+        if (tid == 0) { sh.sel_k = mid; sh.cand_n = 0; sh.mcand_n = 0; }
         __syncthreads();
-        sweep_res(res, M, [&](double r) { atomicAdd(&sh.hist[sel_bin<true>(fabs(r - med))], 1u); });
+        K2_STAMP(2, clock64());
+        find_bin(sh, sh.hist, kBins);
+        const uint32_t bin = sh.sel_bin, kk = sh.sel_k, cnt = sh.sel_cnt;
+        const bool med_fast = cnt <= (uint32_t)kCandCap && !(want_lo && kk == 0);
+        double mlo, mhi;
+        if (med_fast) {
+            const double eps = 1e-9;
+            mlo = bin == 0 ? -__builtin_inf() : (double)bin / kBinScale - kBinOffset - eps;
+            mhi = bin == kBins - 1 ? __builtin_inf() : (double)(bin + 1) / kBinScale - kBinOffset + eps;
+        } else {
+            med = block_median<false>(sh, res, M, n, 0.0);
+            mlo = mhi = med;
+            // the exact path may have reused sh.hist for radix digits: rebuild the value histogram
+            for (int i = tid; i < kBins; i += kSelThreads) sh.hist[i] = 0;
+            __syncthreads();
+            sweep_keys(keys, M8, [&](int, uint32_t q) { atomicAdd(&sh.hist[q >> 4], 1u); });
+            __syncthreads();
+            K2_STAMP(10, 1000000 + cnt);
+        }
+        K2_STAMP(3, clock64());
+        // ---- MAD bracket from the value histogram
+        for (int j = tid; j < kBins; j += kSelThreads) {
+            const uint32_t c = sh.hist[j];
+            if (c) {
+                double dlo, dhi;
+                bin_dist(j, mlo, mhi, dlo, dhi);
+                atomicAdd(&sh.hlo[sel_bin<true>(dlo)], c);
+                atomicAdd(&sh.hhi[sel_bin<true>(dhi)], c);
+            }
+        }
+        if (tid == 0) sh.sel_k = mid;
         __syncthreads();
-        mad = block_median<true>(sh, res, M, n, med);
+        find_bin(sh, sh.hlo, kBins);
+        const uint32_t blo = sh.sel_bin;
+        if (tid == 0) sh.sel_k = mid;
+        __syncthreads();
+        find_bin(sh, sh.hhi, kBins);
+        const uint32_t bhi = sh.sel_bin;
+        const double L0 = (double)blo / kBinScale;
+        const double U0 = bhi >= (uint32_t)(kBins - 1) ? __builtin_inf() : (double)(bhi + 1) / kBinScale;
+        // bin classes: 0 below (dhi < L0), 1 candidate, 2 above (dlo >= U0).  dlo and dhi are V-shaped in
+        // j around the median bin, so class 0 is one run of bins [C, D] inside the run [A, B] of classes
+        // 0 and 1: candidate bins are [A, B] minus [C, D]
+        uint32_t below = 0, ncand = 0, rA = kBins, rB = 0, rC = kBins, rD = 0;
+        for (int j = tid; j < kBins; j += kSelThreads) {
+            double dlo, dhi;
+            bin_dist(j, mlo, mhi, dlo, dhi);
+            const uint32_t cls = dhi < L0 ? 0u : (dlo < U0 ? 1u : 2u);
+            if (cls != 2) { rA = min(rA, (uint32_t)j); rB = max(rB, (uint32_t)j); }
+            if (cls == 0) { rC = min(rC, (uint32_t)j); rD = max(rD, (uint32_t)j); }
+            below += cls == 0 ? sh.hist[j] : 0u;
+            ncand += cls == 1 ? sh.hist[j] : 0u;
+        }
+        below = wave_sum_u(below);
+        ncand = wave_sum_u(ncand);
+        rA = wave_min_u(rA); rB = wave_max_u(rB); rC = wave_min_u(rC); rD = wave_max_u(rD);
+        if (lane == 0) {
+            sh.ired[wave][0] = below; sh.ired[wave][1] = ncand;
+            sh.rngw[wave][0] = rA; sh.rngw[wave][1] = rB; sh.rngw[wave][2] = rC; sh.rngw[wave][3] = rD;
+        }
+        __syncthreads();
+        below = 0; ncand = 0;
+        for (int w = 0; w < kSelWaves; ++w) {
+            below += sh.ired[w][0]; ncand += sh.ired[w][1];
+            rA = min(rA, sh.rngw[w][0]); rB = max(rB, sh.rngw[w][1]);
+            rC = min(rC, sh.rngw[w][2]); rD = max(rD, sh.rngw[w][3]);
+        }
+        const uint32_t kk2 = mid - below;
+        bool mad_fast = ncand <= (uint32_t)kCandCap && mid >= below && kk2 < ncand;
+        K2_STAMP(4, clock64());
+        // ---- one sweep: median candidates (bin b) and MAD candidates (candidate bins)
+        if (med_fast || mad_fast) {
+            const uint32_t mbin = med_fast ? bin : kBins;  // kBins never matches
+            const uint32_t cA = mad_fast ? rA : kBins;
+            sweep_keys(keys, M8, [&](int s, uint32_t q) {
+                const uint32_t j = q >> 4;
+                if (j == mbin) sh.cand[atomicAdd(&sh.cand_n, 1u)] = __longlong_as_double((long long)s);
+                if (j >= cA && j <= rB && !(j >= rC && j <= rD)) sh.mcand[atomicAdd(&sh.mcand_n, 1u)] = (uint32_t)s;
+            });
+            __syncthreads();
+        }
+        K2_STAMP(5, clock64());
+        if (med_fast) {
+            for (uint32_t i = tid; i < cnt; i += kSelThreads) sh.cand[i] = res[__double_as_longlong(sh.cand[i])];
+            __syncthreads();
+            cand_select(sh, cnt, kk, want_lo);
+            med = want_lo ? (sh.sel_lo + sh.sel_hi) / 2.0 : sh.sel_hi;
+            K2_STAMP(10, cnt);
+            __syncthreads();
+        }
+        K2_STAMP(6, clock64());
+        if (mad_fast) {
+            for (uint32_t i = tid; i < ncand; i += kSelThreads) sh.cand[i] = fabs(res[sh.mcand[i]] - med);
+            __syncthreads();
+            cand_select(sh, ncand, kk2, want_lo);
+            // the neighbour below the order statistic may be a counted (not gathered) slot unless it is >= L0
+            if (want_lo && (kk2 == 0 || sh.sel_lo < L0)) mad_fast = false;
+            else mad = want_lo ? (sh.sel_lo + sh.sel_hi) / 2.0 : sh.sel_hi;
+            K2_STAMP(11, ncand);
+            __syncthreads();
+        }
+        K2_STAMP(7, clock64());
+        if (!mad_fast) {
+            for (int i = tid; i < kBins; i += kSelThreads) sh.hist[i] = 0;
+            __syncthreads();
+            sweep_res(res, M, [&](double r) { atomicAdd(&sh.hist[sel_bin<true>(fabs(r - med))], 1u); });
+            __syncthreads();
+            mad = block_median<true>(sh, res, M, n, med);
+            K2_STAMP(12, 1);
+        }
+        K2_STAMP(8, clock64());
+        K2_STAMP(9, clock64());
     }
     if (tid == 0) {
         double sigma = 1.482602218505602 * mad;
@@ -531,7 +792,6 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
         S.n_ref_vis = nrv;
     }
 }
-
 // ------------------------------------------------------------------ K3: weights, normal-equation partials
 // Same ownership and phases as K1 (ref windows only).  Per pixel slot: Tukey weight of r, dx/dy from the
 // staged ref window, the Jacobian row J = dx * Jimg0 + dy * Jimg1 (src/image_alignment.cpp:186-188)
@@ -774,5 +1034,11 @@ void launch_align(const AlignArgs& a, hipStream_t s) {
 }
 
 int align_max_half() { return 9; }
+
+#if defined(SVO_STAMPS)
+extern "C" int svo_debug_stamps(void* out, size_t bytes) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 }  // namespace svo

@@ -68,13 +68,14 @@ struct svo_align_batch {
     svo_camera cam;
     svo_align_params params;
     int32_t n_pairs, max_f, half, area;
-    int64_t res_stride;
+    int64_t res_stride, key_stride;
+    uint16_t* d_keys;
     svo::LevelGeom geom;
     std::vector<svo::PairDesc> h_pairs;
     std::vector<uint8_t> pair_set;
     svo::PairDesc* d_pairs;
     svo::PairState* d_state;
-    double *d_px, *d_bearing, *d_point, *d_xw, *d_jimg, *d_partials, *d_res, *d_pose_out, *d_err;
+    double *d_px, *d_bearing, *d_point, *d_xw, *d_partials, *d_res, *d_pose_out, *d_err;
     int32_t feat_iters, chunks;
     uint8_t *d_has_point, *d_fvis;
     int32_t* d_status;
@@ -237,7 +238,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
-    void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_jimg,
+    void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_keys,
                     b->d_state, b->d_partials, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -272,7 +273,6 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_point, F * 3 * sizeof(double));
     ALLOC(b->d_has_point, F);
     ALLOC(b->d_xw, F * 3 * sizeof(double));
-    ALLOC(b->d_jimg, F * 12 * sizeof(double));
     ALLOC(b->d_state, sizeof(svo::PairState) * n_pairs);
     {
         b->feat_iters = svo::align_feat_iters();
@@ -282,6 +282,8 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_fvis, F);
     b->res_stride = ((int64_t)max_features * area + 2 + 63) / 64 * 64;
     ALLOC(b->d_res, (size_t)n_pairs * b->res_stride * sizeof(double));
+    b->key_stride = ((int64_t)max_features * area + 7) / 8 * 8;
+    ALLOC(b->d_keys, (size_t)n_pairs * b->key_stride * sizeof(uint16_t));
     ALLOC(b->d_pose_out, (size_t)n_pairs * 7 * sizeof(double));
     ALLOC(b->d_err, (size_t)n_pairs * sizeof(double));
     ALLOC(b->d_status, (size_t)n_pairs * sizeof(int32_t));
@@ -372,7 +374,7 @@ int svo_align_batch_run(svo_align_batch* b) {
     svo::AlignArgs a;
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
-    a.xw = b->d_xw; a.jimg = b->d_jimg; a.state = b->d_state; a.partials = b->d_partials;
+    a.xw = b->d_xw; a.keys = b->d_keys; a.key_stride = b->key_stride; a.state = b->d_state; a.partials = b->d_partials;
     a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
     a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;

@@ -42,11 +42,12 @@ struct AlignArgs {
     const double* point;      // [n_pairs*max_f][3]
     const uint8_t* has_point; // [n_pairs*max_f]
     double* xw;               // scratch [n_pairs*max_f][3]   world point per feature
-    double* jimg;             // scratch [n_pairs*max_f][12]  image Jacobian at the current level
     uint8_t* fvis;            // scratch [n_pairs*max_f]      bit0 ref visible, bit1 cur visible
     double* partials;         // scratch [n_pairs][chunks][28] per-workgroup J^T W J (21) | J^T W r (6) | chi2
     double* res;              // scratch [n_pairs][res_stride] residual per pixel slot (+inf = invisible)
     int64_t res_stride;       // >= max_f*area + 1, even (16-B aligned rows for the 16-B sweeps)
+    uint16_t* keys;           // scratch [n_pairs][key_stride] 16-bit monotone key per slot (0xFFFF = invisible)
+    int64_t key_stride;       // >= max_f*area rounded up to 8 (16-B aligned rows)
     double* pose_out;         // [n_pairs][7]
     double* err_out;          // [n_pairs]
     int32_t* status_out;      // [n_pairs]
