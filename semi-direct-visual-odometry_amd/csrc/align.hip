@@ -132,11 +132,19 @@ struct ResRec {
     int32_t vis, isref;        // bit0 ref visible, bit1 cur visible; feature of the ref (else the lastKF)
 };
 struct WtRec {
-    double ur, vr;
-    uint32_t rbase;
-    int32_t rox, roy, vis;
+    double fx, fy;             // fractional parts of the feature pixel at the level (bilinear weights)
+    uint32_t rbase;            // roy * W + rox of the staged ref window
+    int32_t vis, pad0, pad1;
     double ja[6], jb[6];       // computeImageJac at the world point, level-scaled focal lengths
 };
+
+// 4 consecutive bytes of a staged row starting at byte offset `off` (any alignment): two aligned
+// dword reads and a byte-align funnel shift
+__device__ __forceinline__ uint32_t lds_bytes4(const uint8_t* win, int off) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(win + (off & ~3));
+    return __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(off & 3));  // byte shift
+}
+__device__ __forceinline__ double byte_d(uint32_t v, int i) { return (double)((v >> (8 * i)) & 0xFFu); }
 
 }  // namespace
 
@@ -841,9 +849,10 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
             if (a.fvis[gf] == 3) {
                 vis = 3;
                 const double ur = a.px[2 * gf] * scale, vr = a.px[2 * gf + 1] * scale;
-                const int rox = (int)floor(ur) - G::h - 1, roy = (int)floor(vr) - G::h - 1;
-                R.ur = ur; R.vr = vr; R.rox = rox; R.roy = roy;
-                R.rbase = (uint32_t)(roy * W + rox);
+                const double fur = floor(ur), fvr = floor(vr);
+                R.fx = ur - fur;
+                R.fy = vr - fvr;
+                R.rbase = (uint32_t)(((int)fvr - G::h - 1) * W + (int)fur - G::h - 1);
                 image_jac(V3{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]}, a.fx / dom, a.fy / dom, R.ja, R.jb);
             }
         }
@@ -874,6 +883,10 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
     double acc[32];
 #pragma unroll
     for (int t = 0; t < 32; ++t) acc[t] = 0.0;
+    // Per pixel: Tukey weight, then dx/dy of the ref level at (u + x, v + y) (src/image_alignment.cpp:
+    // 180-183).  The four bilinear samples share the feature's fractional weights, so they are formed
+    // from 8 horizontal interpolants of the 12 window bytes around the pixel (same value as four
+    // separate samples up to rounding).
     auto pixel = [&](int e, double r) {
         const int fl = e / G::A, k = e - fl * G::A;
         const WtRec& R = rec[fl];
@@ -881,26 +894,31 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
         const double tt = 1.0 - (r * r) / c2;
         const double w = tt * tt;
         acc[27] += r * r * w;
-        const int ky = k / G::side - G::h, kx = k - (k / G::side) * G::side - G::h;
-        const double row = R.vr + ky, col = R.ur + kx;
+        const int cy = k / G::side + 1, cx = k - (k / G::side) * G::side + 1;  // window cell of floor(u+x, v+y)
         const uint8_t* wr = win + fl * G::fstride3;
-        const double dx = 0.5 * (bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col + 1, row) -
-                                 bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col - 1, row));
-        const double dy = 0.5 * (bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col, row + 1) -
-                                 bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, col, row - 1));
+        uint32_t q[4];  // rows cy-1 .. cy+2, bytes at cols cx-1 .. cx+2
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = cy - 1 + i;
+            q[i] = lds_bytes4(wr, row * G::pitch + (int)((R.rbase + (uint32_t)(row * W)) & 15u) + cx - 1);
+        }
+        const double fx = R.fx, gx = 1.0 - fx, fy = R.fy, gy = 1.0 - fy;
+        auto hv = [&](int i, int c0) { return gx * byte_d(q[i], c0) + fx * byte_d(q[i], c0 + 1); };
+        const double dx = 0.5 * (gy * (hv(1, 2) - hv(1, 0)) + fy * (hv(2, 2) - hv(2, 0)));
+        const double dy = 0.5 * ((gy * hv(2, 1) + fy * hv(3, 1)) - (gy * hv(0, 1) + fy * hv(1, 1)));
         double J[6], wJ[6];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            J[q] = dx * R.ja[q] + dy * R.jb[q];
-            wJ[q] = w * J[q];
+        for (int q6 = 0; q6 < 6; ++q6) {
+            J[q6] = dx * R.ja[q6] + dy * R.jb[q6];
+            wJ[q6] = w * J[q6];
         }
         int t = 0;
 #pragma unroll
-        for (int q = 0; q < 6; ++q)
+        for (int i = 0; i < 6; ++i)
 #pragma unroll
-            for (int p = 0; p <= q; ++p) acc[t++] += wJ[q] * J[p];
+            for (int j = 0; j <= i; ++j) acc[t++] += wJ[i] * J[j];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) acc[21 + q] += wJ[q] * r;
+        for (int i = 0; i < 6; ++i) acc[21 + i] += wJ[i] * r;
     };
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
