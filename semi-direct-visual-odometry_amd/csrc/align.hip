@@ -223,14 +223,18 @@ __global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs 
     if (tid < G::FPB) {
         ResRec& R = rec[tid];
         int32_t vis = 0;
+        // all of the feature's loads at once (one memory round trip); X_w is only used with a point
+        const int64_t gf = fbase + (tid < nb ? tid : 0);
+        const uint8_t hp = a.has_point[gf];
+        const double pu = a.px[2 * gf], pv = a.px[2 * gf + 1];
+        const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
         if (tid < nb) {
-            const int64_t gf = fbase + tid;
-            if (a.has_point[gf]) {
-                const double ur = a.px[2 * gf] * scale, vr = a.px[2 * gf + 1] * scale;
+            if (hp) {
+                const double ur = pu * scale, vr = pv * scale;
                 const int ui = (int)floor(ur), vi = (int)floor(vr);
                 if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
                     vis = 1;
-                    const V3 cp = se3_act(se3_load(S.pose), V3{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]});
+                    const V3 cp = se3_act(se3_load(S.pose), pw);
                     const double cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
                     const double cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
                     const int cui = (int)floor(cu), cvi = (int)floor(cv);
@@ -844,16 +848,19 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
     if (tid < G::FPB) {
         WtRec& R = rec[tid];
         int32_t vis = 0;
+        const int64_t gf = fbase + (tid < nb ? tid : 0);  // all loads at once (see K1)
+        const uint8_t fv = a.fvis[gf];
+        const double pu = a.px[2 * gf], pv = a.px[2 * gf + 1];
+        const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
         if (tid < nb) {
-            const int64_t gf = fbase + tid;
-            if (a.fvis[gf] == 3) {
+            if (fv == 3) {
                 vis = 3;
-                const double ur = a.px[2 * gf] * scale, vr = a.px[2 * gf + 1] * scale;
+                const double ur = pu * scale, vr = pv * scale;
                 const double fur = floor(ur), fvr = floor(vr);
                 R.fx = ur - fur;
                 R.fy = vr - fvr;
                 R.rbase = (uint32_t)(((int)fvr - G::h - 1) * W + (int)fur - G::h - 1);
-                image_jac(V3{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]}, a.fx / dom, a.fy / dom, R.ja, R.jb);
+                image_jac(pw, a.fx / dom, a.fy / dom, R.ja, R.jb);
             }
         }
         R.vis = vis;
@@ -893,7 +900,7 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
         if (R.vis != 3 || !(fabs(r) <= c)) return;  // w = 0: no H, g or chi2 term (src/optimizer.cpp:502-511)
         const double tt = 1.0 - (r * r) / c2;
         const double w = tt * tt;
-        acc[27] += r * r * w;
+        acc[27] = fma(r * r, w, acc[27]);
         const int cy = k / G::side + 1, cx = k - (k / G::side) * G::side + 1;  // window cell of floor(u+x, v+y)
         const uint8_t* wr = win + fl * G::fstride3;
         uint32_t q[4];  // rows cy-1 .. cy+2, bytes at cols cx-1 .. cx+2
@@ -903,22 +910,23 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
             q[i] = lds_bytes4(wr, row * G::pitch + (int)((R.rbase + (uint32_t)(row * W)) & 15u) + cx - 1);
         }
         const double fx = R.fx, gx = 1.0 - fx, fy = R.fy, gy = 1.0 - fy;
-        auto hv = [&](int i, int c0) { return gx * byte_d(q[i], c0) + fx * byte_d(q[i], c0 + 1); };
+        auto hv = [&](int i, int c0) { return fma(fx, byte_d(q[i], c0 + 1), gx * byte_d(q[i], c0)); };
         const double dx = 0.5 * (gy * (hv(1, 2) - hv(1, 0)) + fy * (hv(2, 2) - hv(2, 0)));
         const double dy = 0.5 * ((gy * hv(2, 1) + fy * hv(3, 1)) - (gy * hv(0, 1) + fy * hv(1, 1)));
         double J[6], wJ[6];
 #pragma unroll
         for (int q6 = 0; q6 < 6; ++q6) {
-            J[q6] = dx * R.ja[q6] + dy * R.jb[q6];
+            J[q6] = fma(dx, R.ja[q6], dy * R.jb[q6]);
             wJ[q6] = w * J[q6];
         }
+        // fused multiply-adds: the accumulation order already differs from the reference's GEMM
         int t = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i)
 #pragma unroll
-            for (int j = 0; j <= i; ++j) acc[t++] += wJ[i] * J[j];
+            for (int j = 0; j <= i; ++j) { acc[t] = fma(wJ[i], J[j], acc[t]); ++t; }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) acc[21 + i] += wJ[i] * r;
+        for (int i = 0; i < 6; ++i) acc[21 + i] = fma(wJ[i], r, acc[21 + i]);
     };
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
