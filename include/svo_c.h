@@ -139,6 +139,10 @@ int svo_align_batch_set_initial_poses(svo_align_batch* batch, const double* pose
 /* Run every pair.  Asynchronous on the context stream; inputs stay untouched, so repeated runs are
  * identical (the result pose is written to a separate device buffer). */
 int svo_align_batch_run(svo_align_batch* batch);
+/* One run with a hipEvent between consecutive kernel launches (diagnostics; synchronous).  stage_ms[5]
+ * receives the device time per stage summed over the levels: [0] world points + state, [1] residuals,
+ * [2] robust scale, [3] weights + normal equations, [4] LM step.  No reference counterpart. */
+int svo_align_batch_profile(svo_align_batch* batch, float* stage_ms);
 /* Wait for the last run and copy results: poses n_pairs x 7 (the aligned cur->m_absPose), err
  * n_pairs (the RMSE of the finest level, as align() returns), status n_pairs (Optimizer::Status of
  * the finest level).  Any pointer may be NULL. */

@@ -62,6 +62,7 @@ _SIGNATURES = [
                                            c_void_p, c_void_p]),
     ("svo_align_batch_set_initial_poses", c_int32, [c_void_p, c_void_p]),
     ("svo_align_batch_run", c_int32, [c_void_p]),
+    ("svo_align_batch_profile", c_int32, [c_void_p, ctypes.POINTER(ctypes.c_float)]),
     ("svo_align_batch_results", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     ("svo_align_batch_traces", c_int32, [c_void_p, c_int32, c_void_p]),
     ("svo_feature_align", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_int32,

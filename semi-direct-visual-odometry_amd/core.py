@@ -279,6 +279,14 @@ class AlignBatch:
     def run(self):
         check(lib().svo_align_batch_run(self.handle))
 
+    STAGES = ("init", "residual", "scale", "weights", "solve")
+
+    def profile(self):
+        """One synchronous run with events between launches: device ms per stage, summed over levels."""
+        ms = (ctypes.c_float * 5)()
+        check(lib().svo_align_batch_profile(self.handle, ms))
+        return {k: float(v) for k, v in zip(self.STAGES, ms)}
+
     def results(self):
         poses = np.zeros((self.n_pairs, 7))
         err = np.zeros(self.n_pairs)

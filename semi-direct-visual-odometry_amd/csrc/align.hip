@@ -1030,32 +1030,44 @@ __global__ void __launch_bounds__(64) align_solve_kernel(AlignArgs a, int level)
 }
 
 // ------------------------------------------------------------------ launch
+// marks (optional): an event recorded before every launch and after the last one, in launch order
+// K0, then per level K1 K2 K3 K4 (1 + 4 * levels + 1 events)
 template <int kHalf>
-static void launch_all(const AlignArgs& a, hipStream_t s) {
+static void launch_all(const AlignArgs& a, hipStream_t s, hipEvent_t* marks) {
+    int m = 0;
+    auto mark = [&]() {
+        if (marks) (void)hipEventRecord(marks[m++], s);
+    };
     const int64_t nthreads = (int64_t)a.n_pairs * a.max_f;
     const int64_t blocks = (nthreads > a.n_pairs ? nthreads : a.n_pairs) / 256 + 1;
+    mark();
     hipLaunchKernelGGL(align_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
     const unsigned fgrid = (unsigned)((int64_t)a.n_pairs * a.chunks);
     for (int level = a.max_level; level >= a.min_level; --level) {
+        mark();
         hipLaunchKernelGGL(align_residual_kernel<kHalf>, dim3(fgrid), dim3(kFeatThreads), 0, s, a, level);
+        mark();
         hipLaunchKernelGGL(align_scale_kernel, dim3(a.n_pairs), dim3(kSelThreads), 0, s, a, level);
+        mark();
         hipLaunchKernelGGL(align_weights_kernel<kHalf>, dim3(fgrid), dim3(kFeatThreads), 0, s, a, level);
+        mark();
         hipLaunchKernelGGL(align_solve_kernel, dim3(a.n_pairs), dim3(64), 0, s, a, level);
     }
+    mark();
 }
 
-void launch_align(const AlignArgs& a, hipStream_t s) {
+void launch_align(const AlignArgs& a, hipStream_t s, hipEvent_t* marks) {
     switch (a.half) {
-        case 0: launch_all<0>(a, s); break;
-        case 1: launch_all<1>(a, s); break;
-        case 2: launch_all<2>(a, s); break;
-        case 3: launch_all<3>(a, s); break;
-        case 4: launch_all<4>(a, s); break;
-        case 5: launch_all<5>(a, s); break;
-        case 6: launch_all<6>(a, s); break;
-        case 7: launch_all<7>(a, s); break;
-        case 8: launch_all<8>(a, s); break;
-        default: launch_all<9>(a, s); break;  // the C ABI rejects larger patches
+        case 0: launch_all<0>(a, s, marks); break;
+        case 1: launch_all<1>(a, s, marks); break;
+        case 2: launch_all<2>(a, s, marks); break;
+        case 3: launch_all<3>(a, s, marks); break;
+        case 4: launch_all<4>(a, s, marks); break;
+        case 5: launch_all<5>(a, s, marks); break;
+        case 6: launch_all<6>(a, s, marks); break;
+        case 7: launch_all<7>(a, s, marks); break;
+        case 8: launch_all<8>(a, s, marks); break;
+        default: launch_all<9>(a, s, marks); break;  // the C ABI rejects larger patches
     }
 }
 

@@ -366,7 +366,7 @@ int svo_align_batch_set_initial_poses(svo_align_batch* b, const double* poses) {
     return SVO_OK;
 }
 
-int svo_align_batch_run(svo_align_batch* b) {
+static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     if (!b) return fail(SVO_ERR_ARG, "null argument");
     for (int32_t i = 0; i < b->n_pairs; ++i)
         if (!b->pair_set[i]) return fail(SVO_ERR_STATE, "pair %d was never set", i);
@@ -381,10 +381,36 @@ int svo_align_batch_run(svo_align_batch* b) {
     a.min_level = b->params.min_level; a.max_level = b->params.max_level;
     a.fx = b->cam.fx; a.fy = b->cam.fy; a.cx = b->cam.cx; a.cy = b->cam.cy;
     a.geom = b->geom;
-    svo::launch_align(a, b->ctx->stream);
+    svo::launch_align(a, b->ctx->stream, marks);
     SVO_HIP(hipGetLastError());
     b->ran = true;
     return SVO_OK;
+}
+
+int svo_align_batch_run(svo_align_batch* b) { return run_batch(b, nullptr); }
+
+int svo_align_batch_profile(svo_align_batch* b, float* stage_ms) {
+    if (!b || !stage_ms) return fail(SVO_ERR_ARG, "null argument");
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    const int levels = b->params.max_level - b->params.min_level + 1;
+    const int n = 2 + 4 * levels;
+    std::vector<hipEvent_t> ev(n, nullptr);
+    int rc = SVO_OK;
+    for (int i = 0; i < n && rc == SVO_OK; ++i)
+        if (hipEventCreate(&ev[i]) != hipSuccess) rc = fail(SVO_ERR_HIP, "hipEventCreate failed");
+    if (rc == SVO_OK) rc = run_batch(b, ev.data());
+    if (rc == SVO_OK && hipEventSynchronize(ev[n - 1]) != hipSuccess) rc = fail(SVO_ERR_HIP, "hipEventSynchronize failed");
+    if (rc == SVO_OK) {
+        for (int k = 0; k < 5; ++k) stage_ms[k] = 0.0f;
+        for (int i = 0; i + 1 < n; ++i) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, ev[i], ev[i + 1]) != hipSuccess) { rc = fail(SVO_ERR_HIP, "hipEventElapsedTime failed"); break; }
+            stage_ms[i == 0 ? 0 : 1 + (i - 1) % 4] += ms;
+        }
+    }
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    return rc;
 }
 
 int svo_align_batch_results(svo_align_batch* b, double* poses, double* err, int32_t* status) {

@@ -59,7 +59,7 @@ struct AlignArgs {
     LevelGeom geom;
 };
 
-void launch_align(const AlignArgs& a, hipStream_t s);
+void launch_align(const AlignArgs& a, hipStream_t s, hipEvent_t* marks = nullptr);  // marks: see align.hip
 int align_max_half();  // largest patch half size the alignment kernels are instantiated for
 int align_feat_iters();                                 // feature groups per K1/K3 wave
 int align_chunks(int max_f, int half, int feat_iters);  // K1/K3 workgroups per pair
