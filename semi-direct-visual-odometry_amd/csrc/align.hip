@@ -1,28 +1,29 @@
 // align.hip — sparse image alignment (ImageAlignment::align, src/image_alignment.cpp:25-67) on gfx950.
 //
 // A batch holds n_pairs independent frame pairs.  The coarse-to-fine chain runs as
-// stage kernels over all pairs of the batch, enqueued back to back on the context stream: each stage
-// has its own register budget and launch shape (one persistent kernel spilled ~20 GB/launch).
+// stage kernels over all pairs of the batch, enqueued back to back on the context stream:
 //   K0 init      thread / feature : X_w = T_f^-1 (bearing * |P - C_f|) (:153-155); per-pair state
 //   per level (max..min):
-//   K1 residual  lane group / feature (32 lanes for the 25 px of patch 5, 64 for patch 7): ref
-//                visibility (border rule :140-149), projection pose*X_w into cur (:320-340), image
-//                Jacobian at the WORLD point (:163, :194-248).  The ref window ((2h+5)^2 px) and the
-//                cur window ((2h+3)^2 px) are staged in LDS one row per lane with two aligned 16-B
-//                loads; each lane then samples its pixel: r = I_cur - T_ref (:359) -> per-pair
-//                residual row (+inf = invisible slot)
+//   K1 residual  lane / feature (64-lane workgroups): ref visibility (border rule :140-149), projection
+//                pose * X_w into cur (:320-340); the feature's ref and cur windows are loaded into
+//                registers, one 16-B load per window row, and r = I_cur - T_ref (:359) is formed with the
+//                reference's own bilinear arithmetic in separable form: each window row's horizontal
+//                blends are computed once and shared by the two patch rows that use them (same values,
+//                same rounding as algorithm::bilinearInterpolationDouble, src/algorithm.cpp:896-905)
 //   K2 scale     one workgroup / pair: exact median of the visible r (src/algorithm.cpp:834-853) and of
 //                |r - median| (MAD, :855-865) -> sigma = 1.482602218505602 * MAD (:867-872).  Values
 //                are binned by a monotone map into an LDS histogram; the bin of rank n/2 is exact; one
 //                sweep gathers that bin's values into LDS and ranks them exactly; an overfull bin falls
 //                back to an 11-bit radix select on order-preserving keys
-//   K3 weights   lane group / feature: Tukey weight (src/optimizer.cpp:485-514), chi2 term, dx/dy
-//                re-sampled from the staged ref window; per feature the 5 sums S_xx S_xy S_yy S_xr S_yr
-//                are expanded with the 2x6 image Jacobian (factorised J row = dx*Jimg0 + dy*Jimg1),
-//                one normal-equation term per lane, into per-workgroup partials (fixed order)
-//   K4 solve     one workgroup / pair: partials summed in a fixed order (deterministic, no float
-//                atomics); one lane: Nielsen damping, Eigen-LDLT, pose <- pose * exp(-dx), status,
-//                RMSE (src/optimizer.cpp:279-366, src/image_alignment.cpp:379)
+//   K3 weights   lane / feature: Tukey weight (src/optimizer.cpp:485-514), chi2 term, dx/dy of the ref
+//                level from the register-resident window (:180-183); the lane accumulates the 5 sums
+//                S_xx S_xy S_yy S_xr S_yr of its feature and expands them with the 2x6 image Jacobian
+//                (J row = dx * Jimg0 + dy * Jimg1, :186-188) into the 21 + 6 normal-equation terms; a
+//                halving exchange sums the wave's features into per-workgroup partials.  The last
+//                workgroup of a pair to publish (device-scope arrival counter) sums the partials in a
+//                fixed order (deterministic, no float atomics) and takes the LM step: Nielsen damping,
+//                Eigen-LDLT, pose <- pose * exp(-dx), status, RMSE (src/optimizer.cpp:279-366,
+//                src/image_alignment.cpp:379)
 #include "svo_internal.h"
 #include "svo_math.h"
 
@@ -30,8 +31,7 @@ namespace svo {
 
 namespace {
 
-constexpr int kFeatThreads = 256;    // K1 / K3 workgroup (4 waves)
-constexpr int kFeatWaves = kFeatThreads / 64;
+constexpr int kLaneFeats = 64;       // K1 / K3 workgroup: one wave, one feature per lane
 constexpr int kSelThreads = 512;     // K2 workgroup (two per CU)
 constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kBins = 4096;
@@ -44,10 +44,6 @@ constexpr int kRankCap = 256;        // <= this many candidates: rank counting, 
 constexpr int kRadixBits = 11;
 constexpr double kDblMax = 1.7976931348623157e308;
 
-__device__ __forceinline__ double wave_sum(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    return v;
-}
 __device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
     return v;
@@ -64,49 +60,23 @@ __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
     return v;
 }
-__device__ __forceinline__ void wave_lds_sync() {  // this wave's LDS writes -> visible to its own lanes
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
-// features per K1/K3 workgroup: as many as fit ~40 KB of staged windows, at most 64
-__host__ __device__ constexpr int feats_per_block(int half) {
-    return half <= 3 ? 64 : (half <= 8 ? 32 : 16);
-}
-
+// Window geometry of one feature at one level (patch half size kHalf), in image cells relative to
+// (floor(u), floor(v)) of the feature at that level.
 template <int kHalf>
-struct Geo {
+struct Win {
     static constexpr int h = kHalf, side = 2 * kHalf + 1, A = side * side;
-    static constexpr int RW = 2 * h + 5, CW = 2 * h + 3;               // staged window sides (ref, cur)
-    static constexpr int NB = (RW + 15 + 15) / 16;                     // 16-B blocks per staged row
-    static constexpr int pitch = NB * 16;                              // LDS bytes per staged row
-    static constexpr int FPB = feats_per_block(kHalf);                 // features per workgroup
-    static constexpr int fstride1 = (RW + CW) * pitch + 16;            // K1 bytes per feature (ref + cur)
-    static constexpr int fstride3 = RW * pitch + 16;                   // K3 bytes per feature (ref)
-    static constexpr int pix_iters = (FPB * A + kFeatThreads - 1) / kFeatThreads;
+    static constexpr int RB = 2 * h + 2;           // K1: rows and bytes -h .. h+1 (bilinear corners)
+    static constexpr int WB = 2 * h + 4;           // K3: rows and bytes -h-1 .. h+2 (corners of the +-1 samples)
+    static constexpr int RW = (RB + 3) / 4;        // dwords kept per K1 row
+    static constexpr int WW = (WB + 3) / 4;        // dwords kept per K3 row
+    static constexpr int RD = (RB + 3 + 3) / 4;    // dwords loaded per K1 row (dword-aligned start)
+    static constexpr int WD = (WB + 3 + 3) / 4;    // dwords loaded per K3 row
 };
-
-// bilinearInterpolationDouble (src/algorithm.cpp:896-905) on a staged window.  Row r of the window
-// (top-left pixel (ox, oy), image row pitch W) holds the aligned 16-B blocks that cover image bytes
-// [lin, lin + width), lin = (oy + r) * W + ox = base + r * W, from byte lin & ~15 on.  Bytes past a row's
-// end are the bytes the reference's unchecked Eigen map would read; they only ever carry a zero weight.
-template <int kPitch>
-__device__ __forceinline__ double bilerp_win(const uint8_t* win, uint32_t base, uint32_t W, int ox, int oy, double x,
-                                             double y) {
-    const int32_t x1 = (int32_t)x, y1 = (int32_t)y, x2 = x1 + 1, y2 = y1 + 1;
-    const int ry = y1 - oy, cx = x1 - ox;
-    const uint32_t l1 = base + (uint32_t)ry * W;
-    const uint8_t* r1 = win + ry * kPitch + (int)(l1 & 15u) + cx;
-    const uint8_t* r2 = win + (ry + 1) * kPitch + (int)((l1 + W) & 15u) + cx;
-    const double a = (x2 - x) * r1[0] + (x - x1) * r1[1];
-    const double b = (x2 - x) * r2[0] + (x - x1) * r2[1];
-    return (y2 - y) * a + (y - y1) * b;
-}
 
 // 16-B load from an image plane.  The plane pointers come from the device-resident pair table, so the
 // compiler only sees generic pointers; the explicit global address space keeps these loads off the flat
-// path (a flat load also waits on LDS traffic, which serialises the staging loop).
+// path.  Only 4-B alignment is required (and given).
 __device__ __forceinline__ uint4 gload16(const uint8_t* p) {
 #if defined(__HIP_DEVICE_COMPILE__)
     typedef __attribute__((address_space(1))) const uint4 gu4;
@@ -114,6 +84,59 @@ __device__ __forceinline__ uint4 gload16(const uint8_t* p) {
 #else
     return *reinterpret_cast<const uint4*>(p);  // host pass only parses device code
 #endif
+}
+
+// One window row: image bytes [lin, lin + 4 NW) of `plane` -> out (little-endian dwords), loaded as the
+// ND dwords from the dword below `lin` (16-, 12-, 8- or 4-B global loads) and re-aligned with byte funnel
+// shifts.  Bytes past the row's window are don't-care (the pyramid planes are padded, so the loads stay
+// inside the allocation).
+template <int ND, int NW>
+__device__ __forceinline__ void load_row(const uint8_t* plane, uint32_t lin, uint32_t (&out)[NW]) {
+    uint32_t d[ND + 1];
+    const uint8_t* p = plane + (lin & ~3u);
+#pragma unroll
+    for (int q = 0; q + 4 <= ND; q += 4) {
+        const uint4 v = gload16(p + 4 * q);
+        d[q] = v.x; d[q + 1] = v.y; d[q + 2] = v.z; d[q + 3] = v.w;
+    }
+    constexpr int q0 = ND & ~3;
+#if defined(__HIP_DEVICE_COMPILE__)
+    constexpr int rem = ND & 3;
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    typedef __attribute__((address_space(1))) const u32x3 g3;
+    typedef __attribute__((address_space(1))) const uint2 g2;
+    typedef __attribute__((address_space(1))) const uint32_t g1;
+    if constexpr (rem == 3) { const u32x3 v = *(g3*)(p + 4 * q0); d[q0] = v.x; d[q0 + 1] = v.y; d[q0 + 2] = v.z; }
+    if constexpr (rem == 2) { const uint2 v = *(g2*)(p + 4 * q0); d[q0] = v.x; d[q0 + 1] = v.y; }
+    if constexpr (rem == 1) { d[q0] = *(g1*)(p + 4 * q0); }
+#else
+    for (int q = q0; q < ND; ++q) d[q] = reinterpret_cast<const uint32_t*>(p)[q];
+#endif
+    d[ND] = 0u;
+    const uint32_t sh = lin & 3u;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) out[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+}
+template <int NW>
+__device__ __forceinline__ double wbyte(const uint32_t (&w)[NW], int j) {  // byte j of a row, as double
+    return (double)((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+}
+
+// Raw buffer access to one pair's residual / key rows: the resource (base, size) is wave-uniform, the
+// slot row offset k * fstride goes in the scalar offset and the lane's feature in a 32-bit vector offset,
+// so a slot store / load is one instruction with no per-lane 64-bit address arithmetic.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(const void* base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void slot_store(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void slot_store16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint16_t v) {
+    __builtin_amdgcn_raw_buffer_store_b16(v, rs, (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ double slot_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff, 0));
 }
 
 // 16-bit monotone key of a residual for K2's sweeps: floor((r + 64) * 512) clamped to [0, kKeyMax];
@@ -124,36 +147,26 @@ __device__ __forceinline__ uint16_t res_key(double r) {
     return (uint16_t)(t < 0.0 ? 0u : (t >= (double)kKeyMax ? kKeyMax : (uint32_t)t));
 }
 
-// Per-feature records of K1 / K3 (LDS)
-struct ResRec {
-    double ur, vr, cu, cv;     // feature pixel in the ref level, projection into the cur level
-    int32_t rox, roy, cox, coy;  // staged window origins
-    uint32_t rbase, cbase;     // roy * W + rox, coy * W + cox
-    int32_t vis, isref;        // bit0 ref visible, bit1 cur visible; feature of the ref (else the lastKF)
-};
-struct WtRec {
-    double fx, fy;             // fractional parts of the feature pixel at the level (bilinear weights)
-    uint32_t rbase;            // roy * W + rox of the staged ref window
-    int32_t vis, pad0, pad1;
-    double ja[6], jb[6];       // computeImageJac at the world point, level-scaled focal lengths
-};
-
-// 4 consecutive bytes of a staged row starting at byte offset `off` (any alignment): two aligned
-// dword reads and a byte-align funnel shift
-__device__ __forceinline__ uint32_t lds_bytes4(const uint8_t* win, int off) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(win + (off & ~3));
-    return __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(off & 3));  // byte shift
+// XCD-aware workgroup -> (pair, chunk) map for K1 / K3.  Workgroups are dealt round-robin over the
+// 8 XCDs (b and b + 8 share one), so the workgroups b = 8 s + x of XCD x take pair 8 (s / chunks) + x,
+// chunk s % chunks: every chunk of a pair runs on one XCD, back to back, and the pair's image lines
+// are fetched into one L2 instead of eight.  K2 (one workgroup per pair) lands on the same XCD.  The
+// grid is rounded up to whole groups of 8 pairs; workgroups of pairs >= n_pairs exit.  Placement only
+// affects speed, never results.
+__device__ __forceinline__ void xcd_pair_chunk(int chunks, int& pair, int& chunk) {
+    const int b = (int)blockIdx.x, x = b & 7, s = b >> 3, grp = s / chunks;
+    chunk = s - grp * chunks;
+    pair = grp * 8 + x;
 }
-__device__ __forceinline__ double byte_d(uint32_t v, int i) { return (double)((v >> (8 * i)) & 0xFFu); }
 
 }  // namespace
 
 int align_feat_iters() { return 1; }
 
 int align_chunks(int max_f, int half, int feat_iters) {
+    (void)half;
     (void)feat_iters;
-    const int fpb = feats_per_block(half);
-    return (max_f + fpb - 1) / fpb;
+    return (max_f + kLaneFeats - 1) / kLaneFeats;
 }
 
 // ------------------------------------------------------------------ K0: world points, pair state
@@ -167,9 +180,7 @@ __global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
         S.active = (P.n_ref > 0 && (int64_t)nf * a.area >= 6) ? 1 : 0;
         S.err = P.n_ref == 0 ? 0.0 : -1.0;  // align() returns 0 (:27-28); optimizeLM returns -1 when M < 6
         S.status = P.n_ref == 0 ? kFailed : kNonSuffPoints;
-        const int64_t M = (int64_t)nf * a.area;
-        if (M & 1) a.res[gid * a.res_stride + M] = __builtin_inf();  // pad for the 16-B sweeps of K2
-        for (int64_t s = M; s < ((M + 7) & ~(int64_t)7); ++s) a.keys[gid * a.key_stride + s] = 0xFFFF;
+        a.arrive[gid] = 0u;
         svo_level_trace* tr = a.traces + gid * (a.max_level + 1);
         for (int l = 0; l <= a.max_level; ++l) {
             svo_level_trace t = {};
@@ -193,113 +204,123 @@ __global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
 }
 
 // ------------------------------------------------------------------ K1: visibility, projection, residuals
-// grid.x = n_pairs * chunks; a workgroup owns FPB consecutive features of one pair.
-//   1. one lane per feature: border tests, projection, window origins -> LDS record
-//   2. one lane per window row: two aligned 16-B loads per row -> LDS (all rows' loads issued first)
-//   3. one lane per pixel slot (flattened feature x pixel): r = I_cur - T_ref -> contiguous residual row
+// One lane per feature slot f of the pair (f < fstride; slots past n_features are written invisible).
+// Per pixel (kx, ky) the reference computes T = bilerpD(I_ref, u + kx, v + ky) and I = bilerpD(I_cur,
+// cu + kx, cv + ky) (src/image_alignment.cpp:169-176, :351-359).  With x = u + kx, x1 = (int)x, the
+// column weights x - x1 and x2 - x = 1 - (x - x1) (both exact for x >= 1) depend on kx only and the row
+// blends a = (x2 - x) I(y, x1) + (x - x1) I(y, x2) on (image row, kx) only, so every window row's blends
+// are formed once and shared by the two patch rows that read them: bit-identical to the per-sample
+// formula whenever x1 = floor(u) + kx and y1 = floor(v) + ky.  A feature where u + kx rounds up to the
+// next integer (x1 = floor(u) + kx + 1) takes the per-pixel path instead.
 template <int kHalf>
-__global__ void __launch_bounds__(kFeatThreads) align_residual_kernel(AlignArgs a, int level) {
-    using G = Geo<kHalf>;
-    constexpr int kRows = G::RW + G::CW;
-    constexpr int kRowIters = (G::FPB * kRows + kFeatThreads - 1) / kFeatThreads;
-    __shared__ __attribute__((aligned(16))) uint8_t win[G::FPB * G::fstride1];
-    __shared__ ResRec rec[G::FPB];
-    const int pair = blockIdx.x / a.chunks, chunk = blockIdx.x - pair * a.chunks;
+__global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual_kernel(AlignArgs a, int level) {
+    using G = Win<kHalf>;
+    constexpr int h = G::h, side = G::side, RB = G::RB, NW = G::RW;
+    int pair, chunk;
+    xcd_pair_chunk(a.chunks, pair, chunk);
+    if (pair >= a.n_pairs) return;
     const PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf, f0 = chunk * G::FPB;
-    if (f0 >= nf) return;
-    const int nb = nf - f0 < G::FPB ? nf - f0 : G::FPB;
-    const int tid = threadIdx.x;
+    const int nf = P.n_ref + P.n_kf, fstride = (nf + 7) & ~7;
+    const int f = chunk * kLaneFeats + (int)threadIdx.x;
+    if (f >= fstride) return;
     const int W = a.geom.w[level], H = a.geom.h[level];
     const int64_t loff = a.geom.off[level];
     const double scale = 1.0 / (double)(1 << level);
-    const int border = G::h + 2;
-    const int64_t fbase = (int64_t)pair * a.max_f + f0;
-    const uint8_t* const ref_plane = P.ref_pyr + loff;
-    const uint8_t* const kf_plane = P.kf_pyr + loff;
-    const uint8_t* const cur_plane = P.cur_pyr + loff;
-    if (tid < G::FPB) {
-        ResRec& R = rec[tid];
-        int32_t vis = 0;
-        // all of the feature's loads at once (one memory round trip); X_w is only used with a point
-        const int64_t gf = fbase + (tid < nb ? tid : 0);
-        const uint8_t hp = a.has_point[gf];
+    const int border = h + 2;
+    // slot (k, f) at res[k * fstride + f] (slot_store: scalar row offset, lane offset)
+    const __amdgpu_buffer_rsrc_t res = slot_rsrc(a.res + (int64_t)pair * a.res_stride, a.res_stride * 8);
+    const __amdgpu_buffer_rsrc_t keys = slot_rsrc(a.keys + (int64_t)pair * a.key_stride, a.key_stride * 2);
+    const uint32_t fo = (uint32_t)f;
+    int vis = 0;
+    double ur = 0.0, vr = 0.0, cu = 0.0, cv = 0.0;
+    if (f < nf) {
+        const int64_t gf = (int64_t)pair * a.max_f + f;
+        const uint8_t hp = a.has_point[gf];  // all of the feature's loads at once (one memory round trip)
         const double pu = a.px[2 * gf], pv = a.px[2 * gf + 1];
         const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
-        if (tid < nb) {
-            if (hp) {
-                const double ur = pu * scale, vr = pv * scale;
-                const int ui = (int)floor(ur), vi = (int)floor(vr);
-                if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
-                    vis = 1;
-                    const V3 cp = se3_act(se3_load(S.pose), pw);
-                    const double cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
-                    const double cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
-                    const int cui = (int)floor(cu), cvi = (int)floor(cv);
-                    if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H)) {
-                        vis = 3;
-                        R.ur = ur; R.vr = vr; R.cu = cu; R.cv = cv;
-                        R.rox = ui - G::h - 1; R.roy = vi - G::h - 1;
-                        R.cox = cui - G::h; R.coy = cvi - G::h;
-                        R.rbase = (uint32_t)((vi - G::h - 1) * W + ui - G::h - 1);
-                        R.cbase = (uint32_t)((cvi - G::h) * W + cui - G::h);
-                    }
+        if (hp) {
+            ur = pu * scale;
+            vr = pv * scale;
+            const int ui = (int)floor(ur), vi = (int)floor(vr);
+            if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
+                vis = 1;
+                const V3 cp = se3_act(se3_load(S.pose), pw);
+                cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
+                cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
+                const int cui = (int)floor(cu), cvi = (int)floor(cv);
+                if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H))
+                    vis = 3;
+            }
+        }
+        a.fvis[gf] = (uint8_t)vis;
+    }
+    if (vis != 3) {
+#pragma unroll
+        for (int k = 0; k < G::A; ++k) {
+            slot_store(res, 8 * fo, 8 * (uint32_t)(k * fstride), __builtin_inf());
+            slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), 0xFFFF);
+        }
+        return;
+    }
+    const uint8_t* const rplane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
+    const uint8_t* const cplane = P.cur_pyr + loff;
+    const int ru = (int)floor(ur), rv = (int)floor(vr), qu = (int)floor(cu), qv = (int)floor(cv);
+    double rwx[side], cwx[side];  // x - x1 per patch column (y - y1 per patch row: formed in the row loop)
+    bool fast = true;
+#pragma unroll
+    for (int k = 0; k < side; ++k) {
+        const double d = (double)(k - h);
+        const double xr = ur + d, xc = cu + d;
+        const int xr1 = (int)xr, xc1 = (int)xc;
+        fast = fast && xr1 == ru + k - h && xc1 == qu + k - h && (int)(vr + d) == rv + k - h && (int)(cv + d) == qv + k - h;
+        rwx[k] = xr - (double)xr1;
+        cwx[k] = xc - (double)xc1;
+    }
+    if (fast) {
+        uint32_t rrow[RB][NW], crow[RB][NW];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            load_row<G::RD>(rplane, (uint32_t)((rv - h + r) * W + (ru - h)), rrow[r]);
+            load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
+        }
+        double rprev[side], cprev[side];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            double rcur[side], ccur[side];
+#pragma unroll
+            for (int kx = 0; kx < side; ++kx) {  // (x2 - x) I(y, x1) + (x - x1) I(y, x2)
+                rcur[kx] = (1.0 - rwx[kx]) * wbyte(rrow[r], kx) + rwx[kx] * wbyte(rrow[r], kx + 1);
+                ccur[kx] = (1.0 - cwx[kx]) * wbyte(crow[r], kx) + cwx[kx] * wbyte(crow[r], kx + 1);
+            }
+            if (r > 0) {
+                const int ky = r - 1;
+                const double d = (double)(ky - h), yr = vr + d, yc = cv + d;
+                const double rwy = yr - (double)(rv + ky - h), cwy = yc - (double)(qv + ky - h);  // y - y1
+#pragma unroll
+                for (int kx = 0; kx < side; ++kx) {  // (y2 - y) a + (y - y1) b
+                    const double T = (1.0 - rwy) * rprev[kx] + rwy * rcur[kx];
+                    const double I = (1.0 - cwy) * cprev[kx] + cwy * ccur[kx];
+                    const double rv_ = I - T;
+                    const uint32_t k = (uint32_t)((ky * side + kx) * fstride);
+                    slot_store(res, 8 * fo, 8 * k, rv_);
+                    slot_store16(keys, 2 * fo, 2 * k, res_key(rv_));
                 }
             }
-            a.fvis[gf] = (uint8_t)vis;
-            R.isref = f0 + tid < P.n_ref;
+#pragma unroll
+            for (int kx = 0; kx < side; ++kx) { rprev[kx] = rcur[kx]; cprev[kx] = ccur[kx]; }
         }
-        R.vis = vis;
-    }
-    __syncthreads();
-    // every row's loads first (branch-free: rows of features without a window read a harmless in-plane
-    // block), then the LDS stores
-    uint4 blk[kRowIters][G::NB];
-#pragma unroll
-    for (int i = 0; i < kRowIters; ++i) {
-        const int j = tid + i * kFeatThreads;
-        const int fl = j / kRows < G::FPB ? j / kRows : G::FPB - 1, row = j - fl * kRows;
-        const bool ok = rec[fl].vis == 3, isref = row < G::RW;
-        const uint8_t* plane = isref ? (rec[fl].isref ? ref_plane : kf_plane) : cur_plane;
-        const uint32_t lin = !ok ? 0u : (isref ? rec[fl].rbase + (uint32_t)(row * W)
-                                              : rec[fl].cbase + (uint32_t)((row - G::RW) * W));
-        const uint8_t* src = plane + (lin & ~15u);
-#pragma unroll
-        for (int b = 0; b < G::NB; ++b) blk[i][b] = gload16(src + 16 * b);
-    }
-#pragma unroll
-    for (int i = 0; i < kRowIters; ++i) {
-        const int j = tid + i * kFeatThreads, fl = j / kRows, row = j - fl * kRows;
-        if (j < G::FPB * kRows) {
-            uint4* d = reinterpret_cast<uint4*>(win + fl * G::fstride1 + row * G::pitch);
-#pragma unroll
-            for (int b = 0; b < G::NB; ++b) d[b] = blk[i][b];
-        }
-    }
-    __syncthreads();
-    double* __restrict__ res = a.res + (int64_t)pair * a.res_stride + (int64_t)f0 * G::A;
-    uint16_t* __restrict__ keys = a.keys + (int64_t)pair * a.key_stride + (int64_t)f0 * G::A;
-    const int ne = nb * G::A;
-#pragma unroll 4
-    for (int i = 0; i < G::pix_iters; ++i) {
-        const int e = tid + i * kFeatThreads;
-        if (e < ne) {
-            const int fl = e / G::A, k = e - fl * G::A;
-            const int ky = k / G::side - G::h, kx = k - (k / G::side) * G::side - G::h;
-            const ResRec& R = rec[fl];
-            double r = __builtin_inf();
-            if (R.vis == 3) {
-                const uint8_t* wr = win + fl * G::fstride1;
-                const double T = bilerp_win<G::pitch>(wr, R.rbase, W, R.rox, R.roy, R.ur + kx, R.vr + ky);
-                const double I = bilerp_win<G::pitch>(wr + G::RW * G::pitch, R.cbase, W, R.cox, R.coy, R.cu + kx,
-                                                      R.cv + ky);
-                r = I - T;
+    } else {
+        for (int ky = 0; ky < side; ++ky)
+            for (int kx = 0; kx < side; ++kx) {
+                const double T = bilinear_d(rplane, W, ur + (double)(kx - h), vr + (double)(ky - h));
+                const double I = bilinear_d(cplane, W, cu + (double)(kx - h), cv + (double)(ky - h));
+                const double rv_ = I - T;
+                const uint32_t k = (uint32_t)((ky * side + kx) * fstride);
+                slot_store(res, 8 * fo, 8 * k, rv_);
+                slot_store16(keys, 2 * fo, 2 * k, res_key(rv_));
             }
-            res[e] = r;
-            keys[e] = res_key(r);
-        }
     }
 }
 
@@ -330,8 +351,8 @@ __device__ __forceinline__ int sel_bin(double v) {
     return t < 0.0 ? 0 : (t >= (double)(kBins - 1) ? kBins - 1 : (int)t);
 }
 
-// Sweep the residual row, 4 x 16-B loads in flight per lane; fn(value) for each visible slot.
-// res[M] is +inf when M is odd, so 16-B pairs never read past the row.
+// Sweep the residual row (Ms slots, a multiple of 8), 4 x 16-B loads in flight per lane; fn(value) for
+// each visible slot.
 template <typename Fn>
 __device__ __forceinline__ void sweep_res(const double* __restrict__ res, int M, Fn fn) {
     const int tid = threadIdx.x;
@@ -352,7 +373,7 @@ __device__ __forceinline__ void sweep_res(const double* __restrict__ res, int M,
 
 // Sweep the 16-bit residual keys of K1; fn(slot, key) for each visible slot.  A lane owns kKeyLoads
 // 16-B groups of 8 keys per chunk and issues all of a chunk's loads before using any (one memory round
-// trip per chunk; a config-2 pair, 50 000 slots, is one chunk).  Rows are padded with 0xFFFF to 8.
+// trip per chunk; a config-2 pair, 50 000 slots, is one chunk).  M8 (slots) is a multiple of 8.
 constexpr int kKeyLoads = 13;
 template <typename Fn>
 __device__ __forceinline__ void sweep_keys(const uint16_t* __restrict__ keys, int M8, Fn fn) {
@@ -530,7 +551,7 @@ __device__ void cand_select(SelShared& sh, uint32_t n, uint32_t kk, bool want_lo
 
 // radix fallback inside one overfull bin: exact k-th among values v with sel_bin(v) == bin
 template <bool kMad>
-__device__ double radix_in_bin(SelShared& sh, const double* __restrict__ res, int M, uint32_t bin, uint32_t k,
+__device__ double radix_in_bin(SelShared& sh, const double* __restrict__ res, int Ms, uint32_t bin, uint32_t k,
                                double med) {
     const int tid = threadIdx.x;
     if (tid == 0) { sh.sel_prefix = 0; sh.sel_bits = 0; sh.sel_k = k; }
@@ -542,7 +563,7 @@ __device__ double radix_in_bin(SelShared& sh, const double* __restrict__ res, in
         const int shift = 64 - bits - dbits;
         for (int i = tid; i < (1 << dbits); i += kSelThreads) sh.hist[i] = 0;
         __syncthreads();
-        sweep_res(res, M, [&](double r) {
+        sweep_res(res, Ms, [&](double r) {
             const double v = sel_val<kMad>(r, med);
             if ((uint32_t)sel_bin<kMad>(v) != bin) return;
             const uint64_t key = dkey(v);
@@ -564,12 +585,12 @@ __device__ double radix_in_bin(SelShared& sh, const double* __restrict__ res, in
 
 // (k-1)-th order statistic from the k-th (hi): hi itself if at most k-1 values are < hi, else max(<hi)
 template <bool kMad>
-__device__ double lower_neighbour_sweep(SelShared& sh, const double* __restrict__ res, int M, uint32_t k, double hi,
+__device__ double lower_neighbour_sweep(SelShared& sh, const double* __restrict__ res, int Ms, uint32_t k, double hi,
                                         double med) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t less = 0;
     double mx = -__builtin_inf();
-    sweep_res(res, M, [&](double r) {
+    sweep_res(res, Ms, [&](double r) {
         const double v = sel_val<kMad>(r, med);
         if (v < hi) { ++less; mx = fmax(mx, v); }
     });
@@ -585,9 +606,10 @@ __device__ double lower_neighbour_sweep(SelShared& sh, const double* __restrict_
 }
 
 // computeMedian(v, n) with exact order statistics (odd/even decided by the TOTAL length M,
-// src/algorithm.cpp:845-851; mid == 0 reads vec[mid]).  sh.hist holds the value-bin histogram.
+// src/algorithm.cpp:845-851; mid == 0 reads vec[mid]); Ms = slots swept.  sh.hist holds the value-bin
+// histogram.
 template <bool kMad>
-__device__ double block_median(SelShared& sh, const double* __restrict__ res, int M, uint32_t n, double med) {
+__device__ double block_median(SelShared& sh, const double* __restrict__ res, int M, int Ms, uint32_t n, double med) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t mid = n / 2;
     const bool want_lo = ((M & 1) == 0) && mid > 0;
@@ -598,7 +620,7 @@ __device__ double block_median(SelShared& sh, const double* __restrict__ res, in
     double hi, lo = 0.0;
     if (cnt <= (uint32_t)kCandCap) {
         double below = -__builtin_inf();
-        sweep_res(res, M, [&](double r) {
+        sweep_res(res, Ms, [&](double r) {
             const double v = sel_val<kMad>(r, med);
             const uint32_t b = (uint32_t)sel_bin<kMad>(v);
             if (b == bin) sh.cand[atomicAdd(&sh.cand_n, 1u)] = v;
@@ -614,8 +636,8 @@ __device__ double block_median(SelShared& sh, const double* __restrict__ res, in
         if (want_lo) lo = kk > 0 ? sh.sel_lo : tb;
         __syncthreads();
     } else {
-        hi = radix_in_bin<kMad>(sh, res, M, bin, kk, med);
-        if (want_lo) lo = lower_neighbour_sweep<kMad>(sh, res, M, mid, hi, med);
+        hi = radix_in_bin<kMad>(sh, res, Ms, bin, kk, med);
+        if (want_lo) lo = lower_neighbour_sweep<kMad>(sh, res, Ms, mid, hi, med);
     }
     return want_lo ? (lo + hi) / 2.0 : hi;
 }
@@ -653,7 +675,7 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
     PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf, M = nf * a.area, M8 = (M + 7) & ~7;
+    const int nf = P.n_ref + P.n_kf, M = nf * a.area, M8 = ((nf + 7) & ~7) * a.area;  // M: reference length
     const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
     const uint16_t* __restrict__ keys = a.keys + (int64_t)pair * a.key_stride;
     const uint8_t* __restrict__ fvis = a.fvis + (int64_t)pair * a.max_f;
@@ -690,7 +712,7 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
             mlo = bin == 0 ? -__builtin_inf() : (double)bin / kBinScale - kBinOffset - eps;
             mhi = bin == kBins - 1 ? __builtin_inf() : (double)(bin + 1) / kBinScale - kBinOffset + eps;
         } else {
-            med = block_median<false>(sh, res, M, n, 0.0);
+            med = block_median<false>(sh, res, M, M8, n, 0.0);
             mlo = mhi = med;
             // the exact path may have reused sh.hist for radix digits: rebuild the value histogram
             for (int i = tid; i < kBins; i += kSelThreads) sh.hist[i] = 0;
@@ -785,9 +807,9 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
         if (!mad_fast) {
             for (int i = tid; i < kBins; i += kSelThreads) sh.hist[i] = 0;
             __syncthreads();
-            sweep_res(res, M, [&](double r) { atomicAdd(&sh.hist[sel_bin<true>(fabs(r - med))], 1u); });
+            sweep_res(res, M8, [&](double r) { atomicAdd(&sh.hist[sel_bin<true>(fabs(r - med))], 1u); });
             __syncthreads();
-            mad = block_median<true>(sh, res, M, n, med);
+            mad = block_median<true>(sh, res, M, M8, n, med);
             K2_STAMP(12, 1);
         }
         K2_STAMP(8, clock64());
@@ -804,138 +826,175 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
         S.n_ref_vis = nrv;
     }
 }
-// ------------------------------------------------------------------ K3: weights, normal-equation partials
-// Same ownership and phases as K1 (ref windows only).  Per pixel slot: Tukey weight of r, dx/dy from the
-// staged ref window, the Jacobian row J = dx * Jimg0 + dy * Jimg1 (src/image_alignment.cpp:186-188)
-// and its weighted outer product accumulated in registers (21 H terms, 6 g terms, chi2).  A lane's
-// accumulators are then combined by a halving exchange (32 shuffles for 28 terms) and per-wave sums are
-// added in a fixed order: the partials of a workgroup are deterministic.
+// ------------------------------------------------------------------ K3: weights, normal equations, LM step
+namespace {
+struct SolveShared {
+    double tot[28];
+    double A[36];
+    double tmp[6];
+    int32_t perm[6];
+};
+
+// Per-pair LM step of one level (src/optimizer.cpp:279-366) from the chunk partials, summed in a fixed
+// order: lanes 0..27 one term each, then lane 0 solves.  Called by the one workgroup (one wave) of the
+// pair that published last.
+__device__ void pair_step(const AlignArgs& a, PairState& S, int level, int pair, SolveShared& sh) {
+    const int lane = threadIdx.x;
+    if (lane < 28) {
+        const double* p = a.partials + (int64_t)pair * a.chunks * 28 + lane;
+        double s = 0.0;
+        for (int c = 0; c < a.chunks; ++c) s += p[c * 28];
+        sh.tot[lane] = s;
+    }
+    __syncthreads();
+    if (lane != 0) return;
+    double g[6], dx[6];
+    int q = 0;
+    for (int r = 0; r < 6; ++r)
+        for (int cidx = 0; cidx <= r; ++cidx) {
+            const double v = sh.tot[q++];
+            sh.A[r * 6 + cidx] = v;
+            sh.A[cidx * 6 + r] = v;
+        }
+    for (int r = 0; r < 6; ++r) g[r] = sh.tot[21 + r];
+    const double chi = sh.tot[27];
+    double mx = sh.A[0];
+    for (int r = 1; r < 6; ++r) mx = fmax(mx, sh.A[r * 7]);
+    const double lambda = 1e-2 * mx;  // Nielsen initial damping, first (only) iteration (:294-302)
+    for (int r = 0; r < 6; ++r) sh.A[r * 7] += lambda;
+    svo_level_trace& t = a.traces[(int64_t)pair * (a.max_level + 1) + level];
+    for (int r = 0; r < 36; ++r) t.H[r] = sh.A[r];
+    ldlt_solve_ws(6, sh.A, g, dx, sh.perm, sh.tmp);
+    double m[6];
+    for (int r = 0; r < 6; ++r) m[r] = -dx[r];
+    const SE3 np = se3_compose(se3_load(S.pose), se3_exp(m));  // pose * exp(-dx) (src/image_alignment.cpp:379)
+    se3_store(np, S.pose);
+    bool big = false, nan = false;
+    for (int r = 0; r < 6; ++r) { big |= dx[r] > 1e3; nan |= isnan(dx[r]); }
+    int32_t st = kSuccess;
+    if (big) st = kMaxCoffDx;
+    else if (nan) st = kNonInDx;
+    else {
+        double step = 0.0;
+        for (int r = 0; r < 6; ++r) step += dx[r] * dx[r];
+        st = step < 1e-16 ? kSmallStepSize : st;
+        st = fabs(lambda) >= 1e14 ? kLambdaValue : st;
+    }
+    const double e = sqrt(chi / (double)S.n);  // RMSE before the update (:366)
+    t.level = level; t.n_ref_vis = (int32_t)S.n_ref_vis; t.n_vis = (int32_t)S.n; t.status = st;
+    t.median = S.med; t.mad = S.mad; t.sigma = S.sigma; t.chi2 = chi; t.lambda = lambda; t.err = e;
+    for (int r = 0; r < 6; ++r) { t.g[r] = g[r]; t.dx[r] = dx[r]; }
+    S.err = e;
+    S.status = st;
+    if (level == a.min_level) {
+        for (int i = 0; i < 7; ++i) a.pose_out[7 * pair + i] = S.pose[i];
+        a.err_out[pair] = S.err;
+        a.status_out[pair] = S.status;
+    }
+    a.arrive[pair] = 0u;  // next level's K3 (after the kernel boundary) counts from 0 again
+}
+}  // namespace
+
+// One lane per feature slot, 64-lane workgroups (same map as K1).  dx / dy at (u + kx, v + ky) of the
+// ref level are the reference's central differences of bilinear samples (:180-183) formed with the
+// feature's fractional weights shared by all samples (fx = u - floor(u)): the blends hv(R, c) of every
+// window row R are computed once, and D(R) = hv(R, c+1) - hv(R, c-1), P(R) = hv(R, c) give
+//   dx = (gy D(R0) + fy D(R0+1)) / 2,   dy = (gy (P(R0+1) - P(R0-1)) + fy (P(R0+2) - P(R0))) / 2
+// for the pixel's cell (R0, c) (equal to the per-sample formula up to rounding); pixel row ky (R0 = ky + 1)
+// is emitted once row R0 + 2 has been blended.  The Tukey weight uses
+// r^2 / c^2 as r^2 * (1 / c^2) (rounding only); H, g and chi2 match the reference within the tolerances of
+// tests/test_gpu_parity.py.
 template <int kHalf>
-__global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a, int level) {
-    using G = Geo<kHalf>;
-    constexpr int kRowIters = (G::FPB * G::RW + kFeatThreads - 1) / kFeatThreads;
-    __shared__ __attribute__((aligned(16))) uint8_t win[G::FPB * G::fstride3];
-    __shared__ WtRec rec[G::FPB];
-    __shared__ double part[kFeatWaves][28];
-    const int pair = blockIdx.x / a.chunks, chunk = blockIdx.x - pair * a.chunks;
-    const PairState& S = a.state[pair];
-    if (!S.active) return;
-    const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf, f0 = chunk * G::FPB;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (f0 >= nf) {
-        if (tid < 28) a.partials[((int64_t)pair * a.chunks + chunk) * 28 + tid] = 0.0;
+__global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, int level) {
+    using G = Win<kHalf>;
+    constexpr int h = G::h, side = G::side, WB = G::WB, NW = G::WW;
+    __shared__ SolveShared ssh;
+    int pair, chunk;
+    xcd_pair_chunk(a.chunks, pair, chunk);
+    if (pair >= a.n_pairs) return;
+    PairState& S = a.state[pair];
+    const int lane = threadIdx.x;
+    if (!S.active) {  // nothing to align: the outputs are the initial state (K0)
+        if (level == a.min_level && chunk == 0 && lane == 0) {
+            for (int i = 0; i < 7; ++i) a.pose_out[7 * pair + i] = S.pose[i];
+            a.err_out[pair] = S.err;
+            a.status_out[pair] = S.status;
+        }
         return;
     }
-    const int nb = nf - f0 < G::FPB ? nf - f0 : G::FPB;
+    const PairDesc& P = a.pairs[pair];
+    const int nf = P.n_ref + P.n_kf, fstride = (nf + 7) & ~7;
+    const int f = chunk * kLaneFeats + lane;
     const int W = a.geom.w[level];
     const int64_t loff = a.geom.off[level];
     const double dom = (double)(1 << level), scale = 1.0 / dom;
-    const double c = S.c, c2 = c * c;
-    const int64_t fbase = (int64_t)pair * a.max_f + f0;
-    const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride + (int64_t)f0 * G::A;
-    const int ne = nb * G::A;
-    const uint8_t* const ref_plane = P.ref_pyr + loff;
-    const uint8_t* const kf_plane = P.kf_pyr + loff;
-    // the first kPre residuals of this lane, loaded before the setup so their latency overlaps it
-    constexpr int kPre = G::pix_iters < 8 ? G::pix_iters : 8;
-    double rr[kPre];
-#pragma unroll
-    for (int i = 0; i < kPre; ++i) {
-        const int e = tid + i * kFeatThreads;
-        rr[i] = e < ne ? res[e] : 0.0;
-    }
-    if (tid < G::FPB) {
-        WtRec& R = rec[tid];
-        int32_t vis = 0;
-        const int64_t gf = fbase + (tid < nb ? tid : 0);  // all loads at once (see K1)
-        const uint8_t fv = a.fvis[gf];
-        const double pu = a.px[2 * gf], pv = a.px[2 * gf + 1];
-        const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
-        if (tid < nb) {
-            if (fv == 3) {
-                vis = 3;
-                const double ur = pu * scale, vr = pv * scale;
-                const double fur = floor(ur), fvr = floor(vr);
-                R.fx = ur - fur;
-                R.fy = vr - fvr;
-                R.rbase = (uint32_t)(((int)fvr - G::h - 1) * W + (int)fur - G::h - 1);
-                image_jac(pw, a.fx / dom, a.fy / dom, R.ja, R.jb);
-            }
-        }
-        R.vis = vis;
-    }
-    __syncthreads();
-    uint4 blk[kRowIters][G::NB];  // all loads first, then the LDS stores (see K1)
-#pragma unroll
-    for (int i = 0; i < kRowIters; ++i) {
-        const int j = tid + i * kFeatThreads;
-        const int fl = j / G::RW < G::FPB ? j / G::RW : G::FPB - 1, row = j - fl * G::RW;
-        const uint8_t* plane = f0 + fl < P.n_ref ? ref_plane : kf_plane;
-        const uint32_t lin = rec[fl].vis == 3 ? rec[fl].rbase + (uint32_t)(row * W) : 0u;
-        const uint8_t* src = plane + (lin & ~15u);
-#pragma unroll
-        for (int b = 0; b < G::NB; ++b) blk[i][b] = gload16(src + 16 * b);
-    }
-#pragma unroll
-    for (int i = 0; i < kRowIters; ++i) {
-        const int j = tid + i * kFeatThreads, fl = j / G::RW, row = j - fl * G::RW;
-        if (j < G::FPB * G::RW) {
-            uint4* d = reinterpret_cast<uint4*>(win + fl * G::fstride3 + row * G::pitch);
-#pragma unroll
-            for (int b = 0; b < G::NB; ++b) d[b] = blk[i][b];
-        }
-    }
-    __syncthreads();
+    const double c = S.c, inv_c2 = 1.0 / (c * c);
     double acc[32];
 #pragma unroll
     for (int t = 0; t < 32; ++t) acc[t] = 0.0;
-    // Per pixel: Tukey weight, then dx/dy of the ref level at (u + x, v + y) (src/image_alignment.cpp:
-    // 180-183).  The four bilinear samples share the feature's fractional weights, so they are formed
-    // from 8 horizontal interpolants of the 12 window bytes around the pixel (same value as four
-    // separate samples up to rounding).
-    auto pixel = [&](int e, double r) {
-        const int fl = e / G::A, k = e - fl * G::A;
-        const WtRec& R = rec[fl];
-        if (R.vis != 3 || !(fabs(r) <= c)) return;  // w = 0: no H, g or chi2 term (src/optimizer.cpp:502-511)
-        const double tt = 1.0 - (r * r) / c2;
-        const double w = tt * tt;
-        acc[27] = fma(r * r, w, acc[27]);
-        const int cy = k / G::side + 1, cx = k - (k / G::side) * G::side + 1;  // window cell of floor(u+x, v+y)
-        const uint8_t* wr = win + fl * G::fstride3;
-        uint32_t q[4];  // rows cy-1 .. cy+2, bytes at cols cx-1 .. cx+2
+    const int64_t gf = (int64_t)pair * a.max_f + (f < nf ? f : 0);
+    const uint8_t fvis = f < nf ? a.fvis[gf] : 0;
+    if (fvis == 3) {
+        const double pu = a.px[2 * gf], pv = a.px[2 * gf + 1];
+        const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
+        const __amdgpu_buffer_rsrc_t rr = slot_rsrc(a.res + (int64_t)pair * a.res_stride, a.res_stride * 8);
+        const uint32_t fo = (uint32_t)f;
+        const double ur = pu * scale, vr = pv * scale, fur = floor(ur), fvr = floor(vr);
+        const double fx = ur - fur, gx = 1.0 - fx, fy = vr - fvr, gy = 1.0 - fy;
+        const int ru = (int)fur, rv = (int)fvr;
+        const uint8_t* const plane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
+        uint32_t row[WB][NW];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = cy - 1 + i;
-            q[i] = lds_bytes4(wr, row * G::pitch + (int)((R.rbase + (uint32_t)(row * W)) & 15u) + cx - 1);
-        }
-        const double fx = R.fx, gx = 1.0 - fx, fy = R.fy, gy = 1.0 - fy;
-        auto hv = [&](int i, int c0) { return fma(fx, byte_d(q[i], c0 + 1), gx * byte_d(q[i], c0)); };
-        const double dx = 0.5 * (gy * (hv(1, 2) - hv(1, 0)) + fy * (hv(2, 2) - hv(2, 0)));
-        const double dy = 0.5 * ((gy * hv(2, 1) + fy * hv(3, 1)) - (gy * hv(0, 1) + fy * hv(1, 1)));
-        double J[6], wJ[6];
+        for (int R = 0; R < WB; ++R) load_row<G::WD>(plane, (uint32_t)((rv - h - 1 + R) * W + (ru - h - 1)), row[R]);
+        double sxx = 0.0, sxy = 0.0, syy = 0.0, sxr = 0.0, syr = 0.0, chi = 0.0;
+        double P3[side], P2[side], P1[side], P0[side], D2[side], D1[side], D0[side];  // P(R-3..R), D(R-2..R)
 #pragma unroll
-        for (int q6 = 0; q6 < 6; ++q6) {
-            J[q6] = fma(dx, R.ja[q6], dy * R.jb[q6]);
-            wJ[q6] = w * J[q6];
+        for (int R = 0; R < WB; ++R) {
+            double hv[2 * h + 3];
+#pragma unroll
+            for (int cc = 0; cc < 2 * h + 3; ++cc) hv[cc] = fma(fx, wbyte(row[R], cc + 1), gx * wbyte(row[R], cc));
+#pragma unroll
+            for (int kx = 0; kx < side; ++kx) {
+                P3[kx] = P2[kx]; P2[kx] = P1[kx]; P1[kx] = P0[kx];
+                P0[kx] = hv[kx + 1];  // window column of cell floor(u) + kx - h
+                D2[kx] = D1[kx];
+                D1[kx] = D0[kx];
+                D0[kx] = hv[kx + 2] - hv[kx];
+            }
+            if (R >= 3) {  // pixel row ky: cell row R0 = ky + 1 = R - 2
+                const int ky = R - 3;
+#pragma unroll
+                for (int kx = 0; kx < side; ++kx) {
+                    const double r = slot_load(rr, 8 * fo, 8 * (uint32_t)((ky * side + kx) * fstride));
+                    const double dx = 0.5 * (gy * D2[kx] + fy * D1[kx]);
+                    const double dy = 0.5 * (gy * (P1[kx] - P3[kx]) + fy * (P0[kx] - P2[kx]));
+                    const double r2 = r * r;
+                    const double tt = 1.0 - r2 * inv_c2;
+                    const double w = fabs(r) <= c ? tt * tt : 0.0;  // Tukey (src/optimizer.cpp:502-511)
+                    const double wdx = w * dx, wdy = w * dy;
+                    sxx = fma(wdx, dx, sxx);
+                    sxy = fma(wdx, dy, sxy);
+                    syy = fma(wdy, dy, syy);
+                    sxr = fma(wdx, r, sxr);
+                    syr = fma(wdy, r, syr);
+                    chi = fma(r2, w, chi);
+                }
+            }
         }
-        // fused multiply-adds: the accumulation order already differs from the reference's GEMM
+        // J row = dx * Jimg0 + dy * Jimg1 (image Jacobian at the WORLD point, :163, :194-248): the 21 lower
+        // H terms (row-major lower triangle), the 6 g terms and chi2 of this feature
+        double ja[6], jb[6];
+        image_jac(pw, a.fx / dom, a.fy / dom, ja, jb);
         int t = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i)
 #pragma unroll
-            for (int j = 0; j <= i; ++j) { acc[t] = fma(wJ[i], J[j], acc[t]); ++t; }
+            for (int j = 0; j <= i; ++j) {
+                acc[t++] = (ja[i] * ja[j]) * sxx + (ja[i] * jb[j] + jb[i] * ja[j]) * sxy + (jb[i] * jb[j]) * syy;
+            }
 #pragma unroll
-        for (int i = 0; i < 6; ++i) acc[21 + i] = fma(wJ[i], r, acc[21 + i]);
-    };
-#pragma unroll
-    for (int i = 0; i < kPre; ++i) {
-        const int e = tid + i * kFeatThreads;
-        if (e < ne) pixel(e, rr[i]);
-    }
-    for (int i = kPre; i < G::pix_iters; ++i) {
-        const int e = tid + i * kFeatThreads;
-        if (e < ne) pixel(e, res[e]);
+        for (int i = 0; i < 6; ++i) acc[21 + i] = ja[i] * sxr + jb[i] * syr;
+        acc[27] = chi;
     }
     // halving exchange: after the steps of offsets 32..2 lane L holds term L >> 1 (half of it)
 #pragma unroll
@@ -949,89 +1008,27 @@ __global__ void __launch_bounds__(kFeatThreads) align_weights_kernel(AlignArgs a
         }
     }
     acc[0] += __shfl_xor(acc[0], 1, 64);
-    if ((lane & 1) == 0 && (lane >> 1) < 28) part[wave][lane >> 1] = acc[0];
+    // publish (MI355X_MICROARCH.md, inter-workgroup visibility): the partials are stored write-through
+    // (agent-scope stores: sc1, they leave the XCD's L2), drained by the wave's vmcnt(0), then one lane adds
+    // to the pair's arrival counter; the workgroup whose add returns a.chunks - 1 is the last, acquires
+    // (invalidates its CU's L1) and takes the LM step.  No per-workgroup L2 write-back (release fence).
+    if ((lane & 1) == 0 && (lane >> 1) < 28)
+        __hip_atomic_store(a.partials + ((int64_t)pair * a.chunks + chunk) * 28 + (lane >> 1), acc[0], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t prev = 0;
+    if (lane == 0) prev = __hip_atomic_fetch_add(a.arrive + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __shfl(prev, 0, 64);
+    if (prev != (uint32_t)a.chunks - 1) return;
+    if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid < 28) {
-        double s = 0.0;
-        for (int w = 0; w < kFeatWaves; ++w) s += part[w][tid];
-        a.partials[((int64_t)pair * a.chunks + chunk) * 28 + tid] = s;
-    }
-}
-
-// ------------------------------------------------------------------ K4: normal equations, LM step
-namespace {
-struct SolveShared {
-    double tot[28];
-    double A[36];
-    double tmp[6];
-    int32_t perm[6];
-};
-}  // namespace
-
-__global__ void __launch_bounds__(64) align_solve_kernel(AlignArgs a, int level) {
-    __shared__ SolveShared sh;
-    const int pair = blockIdx.x, tid = threadIdx.x;
-    PairState& S = a.state[pair];
-    const bool last = level == a.min_level;
-    if (S.active) {
-        if (tid < 28) {  // chunk partials in a fixed order
-            const double* p = a.partials + (int64_t)pair * a.chunks * 28 + tid;
-            double s = 0.0;
-            for (int c = 0; c < a.chunks; ++c) s += p[c * 28];
-            sh.tot[tid] = s;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            double g[6], dx[6];
-            int q = 0;
-            for (int r = 0; r < 6; ++r)
-                for (int cidx = 0; cidx <= r; ++cidx) {
-                    const double v = sh.tot[q++];
-                    sh.A[r * 6 + cidx] = v;
-                    sh.A[cidx * 6 + r] = v;
-                }
-            for (int r = 0; r < 6; ++r) g[r] = sh.tot[21 + r];
-            const double chi = sh.tot[27];
-            double mx = sh.A[0];
-            for (int r = 1; r < 6; ++r) mx = fmax(mx, sh.A[r * 7]);
-            const double lambda = 1e-2 * mx;
-            for (int r = 0; r < 6; ++r) sh.A[r * 7] += lambda;
-            svo_level_trace& t = a.traces[(int64_t)pair * (a.max_level + 1) + level];
-            for (int r = 0; r < 36; ++r) t.H[r] = sh.A[r];
-            ldlt_solve_ws(6, sh.A, g, dx, sh.perm, sh.tmp);
-            double m[6];
-            for (int r = 0; r < 6; ++r) m[r] = -dx[r];
-            const SE3 np = se3_compose(se3_load(S.pose), se3_exp(m));
-            se3_store(np, S.pose);
-            bool big = false, nan = false;
-            for (int r = 0; r < 6; ++r) { big |= dx[r] > 1e3; nan |= isnan(dx[r]); }
-            int32_t st = kSuccess;
-            if (big) st = kMaxCoffDx;
-            else if (nan) st = kNonInDx;
-            else {
-                double step = 0.0;
-                for (int r = 0; r < 6; ++r) step += dx[r] * dx[r];
-                st = step < 1e-16 ? kSmallStepSize : st;
-                st = fabs(lambda) >= 1e14 ? kLambdaValue : st;
-            }
-            const double e = sqrt(chi / (double)S.n);
-            t.level = level; t.n_ref_vis = (int32_t)S.n_ref_vis; t.n_vis = (int32_t)S.n; t.status = st;
-            t.median = S.med; t.mad = S.mad; t.sigma = S.sigma; t.chi2 = chi; t.lambda = lambda; t.err = e;
-            for (int r = 0; r < 6; ++r) { t.g[r] = g[r]; t.dx[r] = dx[r]; }
-            S.err = e;
-            S.status = st;
-        }
-    }
-    if (last && tid == 0) {
-        for (int i = 0; i < 7; ++i) a.pose_out[7 * pair + i] = S.pose[i];
-        a.err_out[pair] = S.err;
-        a.status_out[pair] = S.status;
-    }
+    pair_step(a, S, level, pair, ssh);
 }
 
 // ------------------------------------------------------------------ launch
 // marks (optional): an event recorded before every launch and after the last one, in launch order
-// K0, then per level K1 K2 K3 K4 (1 + 4 * levels + 1 events)
+// K0, then per level K1 K2 K3 (1 + 3 * levels + 1 events)
 template <int kHalf>
 static void launch_all(const AlignArgs& a, hipStream_t s, hipEvent_t* marks) {
     int m = 0;
@@ -1042,16 +1039,14 @@ static void launch_all(const AlignArgs& a, hipStream_t s, hipEvent_t* marks) {
     const int64_t blocks = (nthreads > a.n_pairs ? nthreads : a.n_pairs) / 256 + 1;
     mark();
     hipLaunchKernelGGL(align_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
-    const unsigned fgrid = (unsigned)((int64_t)a.n_pairs * a.chunks);
+    const unsigned fgrid = (unsigned)((int64_t)((a.n_pairs + 7) / 8) * 8 * a.chunks);
     for (int level = a.max_level; level >= a.min_level; --level) {
         mark();
-        hipLaunchKernelGGL(align_residual_kernel<kHalf>, dim3(fgrid), dim3(kFeatThreads), 0, s, a, level);
+        hipLaunchKernelGGL(align_residual_kernel<kHalf>, dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
         mark();
         hipLaunchKernelGGL(align_scale_kernel, dim3(a.n_pairs), dim3(kSelThreads), 0, s, a, level);
         mark();
-        hipLaunchKernelGGL(align_weights_kernel<kHalf>, dim3(fgrid), dim3(kFeatThreads), 0, s, a, level);
-        mark();
-        hipLaunchKernelGGL(align_solve_kernel, dim3(a.n_pairs), dim3(64), 0, s, a, level);
+        hipLaunchKernelGGL(align_weights_kernel<kHalf>, dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
     }
     mark();
 }

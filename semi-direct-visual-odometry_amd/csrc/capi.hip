@@ -76,6 +76,7 @@ struct svo_align_batch {
     svo::PairDesc* d_pairs;
     svo::PairState* d_state;
     double *d_px, *d_bearing, *d_point, *d_xw, *d_partials, *d_res, *d_pose_out, *d_err;
+    uint32_t* d_arrive;
     int32_t feat_iters, chunks;
     uint8_t *d_has_point, *d_fvis;
     int32_t* d_status;
@@ -239,7 +240,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_keys,
-                    b->d_state, b->d_partials, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
+                    b->d_state, b->d_partials, b->d_arrive, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -279,10 +280,12 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
         b->chunks = svo::align_chunks(max_features, half, b->feat_iters);
     }
     ALLOC(b->d_partials, (size_t)n_pairs * b->chunks * 28 * sizeof(double));
+    ALLOC(b->d_arrive, (size_t)n_pairs * sizeof(uint32_t));
     ALLOC(b->d_fvis, F);
-    b->res_stride = ((int64_t)max_features * area + 2 + 63) / 64 * 64;
+    const int64_t slots = (int64_t)area * ((max_features + 7) / 8 * 8);  // pixel-major slots, see AlignArgs
+    b->res_stride = (slots + 63) / 64 * 64;
     ALLOC(b->d_res, (size_t)n_pairs * b->res_stride * sizeof(double));
-    b->key_stride = ((int64_t)max_features * area + 7) / 8 * 8;
+    b->key_stride = b->res_stride;
     ALLOC(b->d_keys, (size_t)n_pairs * b->key_stride * sizeof(uint16_t));
     ALLOC(b->d_pose_out, (size_t)n_pairs * 7 * sizeof(double));
     ALLOC(b->d_err, (size_t)n_pairs * sizeof(double));
@@ -375,6 +378,7 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
     a.xw = b->d_xw; a.keys = b->d_keys; a.key_stride = b->key_stride; a.state = b->d_state; a.partials = b->d_partials;
+    a.arrive = b->d_arrive;
     a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
     a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
@@ -393,7 +397,7 @@ int svo_align_batch_profile(svo_align_batch* b, float* stage_ms) {
     if (!b || !stage_ms) return fail(SVO_ERR_ARG, "null argument");
     SVO_HIP(hipSetDevice(b->ctx->device));
     const int levels = b->params.max_level - b->params.min_level + 1;
-    const int n = 2 + 4 * levels;
+    const int n = 2 + 3 * levels;
     std::vector<hipEvent_t> ev(n, nullptr);
     int rc = SVO_OK;
     for (int i = 0; i < n && rc == SVO_OK; ++i)
@@ -405,7 +409,7 @@ int svo_align_batch_profile(svo_align_batch* b, float* stage_ms) {
         for (int i = 0; i + 1 < n; ++i) {
             float ms = 0.0f;
             if (hipEventElapsedTime(&ms, ev[i], ev[i + 1]) != hipSuccess) { rc = fail(SVO_ERR_HIP, "hipEventElapsedTime failed"); break; }
-            stage_ms[i == 0 ? 0 : 1 + (i - 1) % 4] += ms;
+            stage_ms[i == 0 ? 0 : 1 + (i - 1) % 3] += ms;  // [4] stays 0: the LM step runs inside K3
         }
     }
     for (hipEvent_t e : ev)

@@ -44,10 +44,14 @@ struct AlignArgs {
     double* xw;               // scratch [n_pairs*max_f][3]   world point per feature
     uint8_t* fvis;            // scratch [n_pairs*max_f]      bit0 ref visible, bit1 cur visible
     double* partials;         // scratch [n_pairs][chunks][28] per-workgroup J^T W J (21) | J^T W r (6) | chi2
+    uint32_t* arrive;         // scratch [n_pairs] K3 workgroups of the current level that have published partials
+    // Residual slots of a pair are pixel-major: slot (k, f) = k * fstride + f for pixel k of the patch and
+    // feature f, fstride = n_features rounded up to 8 (one lane per feature reads and writes coalesced).
+    // Slots of features >= n_features are invisible.
     double* res;              // scratch [n_pairs][res_stride] residual per pixel slot (+inf = invisible)
-    int64_t res_stride;       // >= max_f*area + 1, even (16-B aligned rows for the 16-B sweeps)
+    int64_t res_stride;       // >= area * round_up(max_f, 8), multiple of 64
     uint16_t* keys;           // scratch [n_pairs][key_stride] 16-bit monotone key per slot (0xFFFF = invisible)
-    int64_t key_stride;       // >= max_f*area rounded up to 8 (16-B aligned rows)
+    int64_t key_stride;       // >= area * round_up(max_f, 8), multiple of 64
     double* pose_out;         // [n_pairs][7]
     double* err_out;          // [n_pairs]
     int32_t* status_out;      // [n_pairs]

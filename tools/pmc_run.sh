@@ -10,7 +10,7 @@ i=0
 for set in "$@"; do
     i=$((i+1))
     echo "== pass $i: $set"
-    timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- $BENCH > gpurun_out/pmc/p$i.log 2>&1
+    timeout -s KILL 150 rocprofv3 --pmc $set --kernel-trace --output-format csv -d gpurun_out/pmc/p$i -o run -- $BENCH > gpurun_out/pmc/p$i.log 2>&1
     rc=$?
     echo "== pass $i rc=$rc"
     if [ "$rc" -ge 124 ]; then exit $rc; fi
