@@ -41,6 +41,7 @@ constexpr double kKeyScale = 512.0;  // K1's 16-bit residual key: 16 keys per va
 constexpr uint32_t kKeyMax = 65534;  // largest key of a visible slot; 0xFFFF = invisible
 constexpr int kCandCap = 2048;
 constexpr int kRankCap = 256;        // <= this many candidates: rank counting, else bitonic sort
+constexpr int kPrevCap = 256;        // slots of the bin below the median's gathered for its lower neighbour
 constexpr int kRadixBits = 11;
 constexpr double kDblMax = 1.7976931348623157e308;
 
@@ -159,6 +160,10 @@ __device__ __forceinline__ void xcd_pair_chunk(int chunks, int& pair, int& chunk
     pair = grp * 8 + x;
 }
 
+// Slot rows of a pair are fstride = n_features rounded up to 64 wide: a wave's 64 keys of one patch pixel
+// are one whole aligned 128-B line.
+__device__ __forceinline__ int slot_stride(int nf) { return (nf + 63) & ~63; }
+
 }  // namespace
 
 int align_feat_iters() { return 1; }
@@ -222,15 +227,14 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual
     const PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf, fstride = (nf + 7) & ~7;
+    const int nf = P.n_ref + P.n_kf, fstride = slot_stride(nf);
     const int f = chunk * kLaneFeats + (int)threadIdx.x;
     if (f >= fstride) return;
     const int W = a.geom.w[level], H = a.geom.h[level];
     const int64_t loff = a.geom.off[level];
     const double scale = 1.0 / (double)(1 << level);
     const int border = h + 2;
-    // slot (k, f) at res[k * fstride + f] (slot_store: scalar row offset, lane offset)
-    const __amdgpu_buffer_rsrc_t res = slot_rsrc(a.res + (int64_t)pair * a.res_stride, a.res_stride * 8);
+    // key of slot (k, f) at keys[k * fstride + f] (slot_store16: scalar row offset, lane offset)
     const __amdgpu_buffer_rsrc_t keys = slot_rsrc(a.keys + (int64_t)pair * a.key_stride, a.key_stride * 2);
     const uint32_t fo = (uint32_t)f;
     int vis = 0;
@@ -250,18 +254,17 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual
                 cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
                 cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
                 const int cui = (int)floor(cu), cvi = (int)floor(cv);
-                if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H))
+                if (!((cui - border) < 0 || (cvi - border) < 0 || (cui + border) >= W || (cvi + border) >= H)) {
                     vis = 3;
+                    reinterpret_cast<double2*>(a.cproj)[gf] = make_double2(cu, cv);
+                }
             }
         }
         a.fvis[gf] = (uint8_t)vis;
     }
     if (vis != 3) {
 #pragma unroll
-        for (int k = 0; k < G::A; ++k) {
-            slot_store(res, 8 * fo, 8 * (uint32_t)(k * fstride), __builtin_inf());
-            slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), 0xFFFF);
-        }
+        for (int k = 0; k < G::A; ++k) slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), 0xFFFF);
         return;
     }
     const uint8_t* const rplane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
@@ -302,10 +305,8 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual
                 for (int kx = 0; kx < side; ++kx) {  // (y2 - y) a + (y - y1) b
                     const double T = (1.0 - rwy) * rprev[kx] + rwy * rcur[kx];
                     const double I = (1.0 - cwy) * cprev[kx] + cwy * ccur[kx];
-                    const double rv_ = I - T;
                     const uint32_t k = (uint32_t)((ky * side + kx) * fstride);
-                    slot_store(res, 8 * fo, 8 * k, rv_);
-                    slot_store16(keys, 2 * fo, 2 * k, res_key(rv_));
+                    slot_store16(keys, 2 * fo, 2 * k, res_key(I - T));
                 }
             }
 #pragma unroll
@@ -316,10 +317,8 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual
             for (int kx = 0; kx < side; ++kx) {
                 const double T = bilinear_d(rplane, W, ur + (double)(kx - h), vr + (double)(ky - h));
                 const double I = bilinear_d(cplane, W, cu + (double)(kx - h), cv + (double)(ky - h));
-                const double rv_ = I - T;
                 const uint32_t k = (uint32_t)((ky * side + kx) * fstride);
-                slot_store(res, 8 * fo, 8 * k, rv_);
-                slot_store16(keys, 2 * fo, 2 * k, res_key(rv_));
+                slot_store16(keys, 2 * fo, 2 * k, res_key(I - T));
             }
     }
 }
@@ -333,12 +332,13 @@ struct SelShared {
     uint32_t hhi[kBins];    // (hhi is reused by cand_select's fine histogram)
     double cand[kCandCap];
     uint32_t mcand[kCandCap];  // MAD candidate slots
+    uint32_t pcand[kPrevCap];  // slots of the highest non-empty bin below the median's (even length, rank 0)
     double small[kRankCap];    // values of one fine bin (cand_select)
     uint32_t scan[kSelWaves];
     uint32_t ired[kSelWaves][2];
     double red[kSelWaves], red2[kSelWaves];
     uint64_t sel_prefix;
-    uint32_t sel_k, sel_cnt, sel_bits, sel_bin, cand_n, mcand_n, small_n;
+    uint32_t sel_k, sel_cnt, sel_bits, sel_bin, cand_n, mcand_n, pcand_n, small_n;
     uint32_t rngw[kSelWaves][4];
     double sel_hi, sel_lo;
 };
@@ -351,10 +351,53 @@ __device__ __forceinline__ int sel_bin(double v) {
     return t < 0.0 ? 0 : (t >= (double)(kBins - 1) ? kBins - 1 : (int)t);
 }
 
-// Sweep the residual row (Ms slots, a multiple of 8), 4 x 16-B loads in flight per lane; fn(value) for
-// each visible slot.
+// The exact residual of one slot, recomputed from the images: K1 keeps only the 16-bit keys and the
+// projection of each visible feature, so K2 evaluates r = bilerpD(I_cur, cu + kx, cv + ky) -
+// bilerpD(I_ref, u + kx, v + ky) (src/image_alignment.cpp:351-359) for the few slots it must rank
+// exactly; the per-sample formula is the one K1's separable form reproduces bit for bit.
+struct SlotSrc {
+    const uint16_t* keys;
+    double* scratch;        // pair's slot row for the exact paths (materialize())
+    const double* px;       // pair's feature pixels (level 0)
+    const double* cproj;    // pair's projections into the cur level (K1)
+    const uint8_t *rplane, *kplane, *cplane;
+    int W, fstride, n_ref, side, half;
+    double scale;
+    __device__ __forceinline__ double r(uint32_t s) const {
+        const int k = (int)(s / (uint32_t)fstride), f = (int)(s - (uint32_t)k * (uint32_t)fstride);
+        const int ky = k / side, kx = k - ky * side;
+        const double ur = px[2 * f] * scale, vr = px[2 * f + 1] * scale;
+        const double cu = cproj[2 * f], cv = cproj[2 * f + 1];
+        const double T = bilinear_d(f < n_ref ? rplane : kplane, W, ur + (double)(kx - half), vr + (double)(ky - half));
+        const double I = bilinear_d(cplane, W, cu + (double)(kx - half), cv + (double)(ky - half));
+        return I - T;
+    }
+};
+
+// Exact residual of every slot (+inf = invisible) into the pair's scratch row, for the exact paths of K2
+// (overfull bins; a neighbour the bin bracket cannot settle): four slots in flight per lane.
+__device__ void materialize(const SlotSrc& res, int Ms) {
+    for (int s0 = threadIdx.x; s0 < Ms; s0 += 4 * kSelThreads) {
+        double v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int s = s0 + u * kSelThreads;
+            v[u] = (s < Ms && res.keys[s] != 0xFFFF) ? res.r((uint32_t)s) : __builtin_inf();
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int s = s0 + u * kSelThreads;
+            if (s < Ms) res.scratch[s] = v[u];
+        }
+    }
+    __syncthreads();
+}
+
+// Sweep the materialized residual row (Ms slots, a multiple of 8), 4 x 16-B loads in flight per lane;
+// fn(value) for each visible slot.
 template <typename Fn>
-__device__ __forceinline__ void sweep_res(const double* __restrict__ res, int M, Fn fn) {
+__device__ __forceinline__ void sweep_res(const SlotSrc& src, int M, Fn fn) {
+    const double* __restrict__ res = src.scratch;
     const int tid = threadIdx.x;
     for (int base = 2 * tid; base < M; base += 8 * kSelThreads) {
         double2 v[4];
@@ -551,7 +594,7 @@ __device__ void cand_select(SelShared& sh, uint32_t n, uint32_t kk, bool want_lo
 
 // radix fallback inside one overfull bin: exact k-th among values v with sel_bin(v) == bin
 template <bool kMad>
-__device__ double radix_in_bin(SelShared& sh, const double* __restrict__ res, int Ms, uint32_t bin, uint32_t k,
+__device__ double radix_in_bin(SelShared& sh, const SlotSrc& res, int Ms, uint32_t bin, uint32_t k,
                                double med) {
     const int tid = threadIdx.x;
     if (tid == 0) { sh.sel_prefix = 0; sh.sel_bits = 0; sh.sel_k = k; }
@@ -585,7 +628,7 @@ __device__ double radix_in_bin(SelShared& sh, const double* __restrict__ res, in
 
 // (k-1)-th order statistic from the k-th (hi): hi itself if at most k-1 values are < hi, else max(<hi)
 template <bool kMad>
-__device__ double lower_neighbour_sweep(SelShared& sh, const double* __restrict__ res, int Ms, uint32_t k, double hi,
+__device__ double lower_neighbour_sweep(SelShared& sh, const SlotSrc& res, int Ms, uint32_t k, double hi,
                                         double med) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t less = 0;
@@ -609,7 +652,7 @@ __device__ double lower_neighbour_sweep(SelShared& sh, const double* __restrict_
 // src/algorithm.cpp:845-851; mid == 0 reads vec[mid]); Ms = slots swept.  sh.hist holds the value-bin
 // histogram.
 template <bool kMad>
-__device__ double block_median(SelShared& sh, const double* __restrict__ res, int M, int Ms, uint32_t n, double med) {
+__device__ double block_median(SelShared& sh, const SlotSrc& res, int M, int Ms, uint32_t n, double med) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t mid = n / 2;
     const bool want_lo = ((M & 1) == 0) && mid > 0;
@@ -668,16 +711,29 @@ __device__ uint64_t g_stamps[4096 * 16];
 //      bins; only those slots' exact residuals are read
 //   4. exact selection among the candidates (rank counting or bitonic sort in LDS)
 // Cases the fast path cannot settle (overfull bins; the even-length neighbour below a bin's first
-// element) take the exact path on the 8-B residuals.
-__global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, int level) {
+// element) take the exact path over every visible slot's recomputed residual.
+__global__ void __launch_bounds__(kSelThreads, 4) align_scale_kernel(AlignArgs a, int level) {
     __shared__ SelShared sh;
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     PairState& S = a.state[pair];
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf, M = nf * a.area, M8 = ((nf + 7) & ~7) * a.area;  // M: reference length
-    const double* __restrict__ res = a.res + (int64_t)pair * a.res_stride;
+    const int nf = P.n_ref + P.n_kf, M = nf * a.area, M8 = slot_stride(nf) * a.area;  // M: reference length
     const uint16_t* __restrict__ keys = a.keys + (int64_t)pair * a.key_stride;
+    SlotSrc res;
+    res.keys = keys;
+    res.scratch = a.scratch + (int64_t)pair * a.key_stride;
+    res.px = a.px + (int64_t)pair * a.max_f * 2;
+    res.cproj = a.cproj + (int64_t)pair * a.max_f * 2;
+    res.rplane = P.ref_pyr + a.geom.off[level];
+    res.kplane = P.kf_pyr + a.geom.off[level];
+    res.cplane = P.cur_pyr + a.geom.off[level];
+    res.W = a.geom.w[level];
+    res.fstride = slot_stride(nf);
+    res.n_ref = P.n_ref;
+    res.half = a.half;
+    res.side = 2 * a.half + 1;
+    res.scale = 1.0 / (double)(1 << level);
     const uint8_t* __restrict__ fvis = a.fvis + (int64_t)pair * a.max_f;
     K2_STAMP(0, clock64());
     uint32_t nrv = 0, ncv = 0;
@@ -700,18 +756,36 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
     if (n > 0) {
         K2_STAMP(1, clock64());
         sweep_keys(keys, M8, [&](int, uint32_t q) { atomicAdd(&sh.hist[q >> 4], 1u); });
-        if (tid == 0) { sh.sel_k = mid; sh.cand_n = 0; sh.mcand_n = 0; }
+        if (tid == 0) { sh.sel_k = mid; sh.cand_n = 0; sh.mcand_n = 0; sh.pcand_n = 0; }
         __syncthreads();
         K2_STAMP(2, clock64());
         find_bin(sh, sh.hist, kBins);
         const uint32_t bin = sh.sel_bin, kk = sh.sel_k, cnt = sh.sel_cnt;
-        const bool med_fast = cnt <= (uint32_t)kCandCap && !(want_lo && kk == 0);
+        // even length with rank n/2 first in its bin: the lower neighbour is the largest value of the
+        // highest non-empty bin below (gathered too)
+        const bool need_prev = want_lo && kk == 0;
+        uint32_t pbin = kBins;
+        if (need_prev) {
+            uint32_t jm = 0;
+            for (int j = tid; j < (int)bin; j += kSelThreads)
+                if (sh.hist[j]) jm = max(jm, (uint32_t)j + 1u);
+            jm = wave_max_u(jm);
+            if (lane == 0) sh.rngw[wave][0] = jm;
+            __syncthreads();
+            jm = 0;
+            for (int w = 0; w < kSelWaves; ++w) jm = max(jm, sh.rngw[w][0]);
+            pbin = jm - 1u;  // mid > 0 values lie below the bin
+        }
+        const bool med_fast = cnt <= (uint32_t)kCandCap && (!need_prev || sh.hist[pbin] <= (uint32_t)kPrevCap);
+        bool mat = false;  // scratch row materialized (block-uniform)
         double mlo, mhi;
         if (med_fast) {
             const double eps = 1e-9;
             mlo = bin == 0 ? -__builtin_inf() : (double)bin / kBinScale - kBinOffset - eps;
             mhi = bin == kBins - 1 ? __builtin_inf() : (double)(bin + 1) / kBinScale - kBinOffset + eps;
         } else {
+            materialize(res, M8);
+            mat = true;
             med = block_median<false>(sh, res, M, M8, n, 0.0);
             mlo = mhi = med;
             // the exact path may have reused sh.hist for radix digits: rebuild the value histogram
@@ -775,26 +849,37 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
         // ---- one sweep: median candidates (bin b) and MAD candidates (candidate bins)
         if (med_fast || mad_fast) {
             const uint32_t mbin = med_fast ? bin : kBins;  // kBins never matches
+            const uint32_t pb = med_fast ? pbin : kBins;
             const uint32_t cA = mad_fast ? rA : kBins;
             sweep_keys(keys, M8, [&](int s, uint32_t q) {
                 const uint32_t j = q >> 4;
                 if (j == mbin) sh.cand[atomicAdd(&sh.cand_n, 1u)] = __longlong_as_double((long long)s);
+                if (j == pb) sh.pcand[atomicAdd(&sh.pcand_n, 1u)] = (uint32_t)s;
                 if (j >= cA && j <= rB && !(j >= rC && j <= rD)) sh.mcand[atomicAdd(&sh.mcand_n, 1u)] = (uint32_t)s;
             });
             __syncthreads();
         }
         K2_STAMP(5, clock64());
         if (med_fast) {
-            for (uint32_t i = tid; i < cnt; i += kSelThreads) sh.cand[i] = res[__double_as_longlong(sh.cand[i])];
+            for (uint32_t i = tid; i < cnt; i += kSelThreads) sh.cand[i] = res.r((uint32_t)__double_as_longlong(sh.cand[i]));
+            double lo_prev = -__builtin_inf();
+            if (need_prev) {
+                const uint32_t pc = sh.hist[pbin];
+                for (uint32_t i = tid; i < pc; i += kSelThreads) lo_prev = fmax(lo_prev, res.r(sh.pcand[i]));
+                lo_prev = wave_max(lo_prev);
+                if (lane == 0) sh.red2[wave] = lo_prev;
+            }
             __syncthreads();
-            cand_select(sh, cnt, kk, want_lo);
-            med = want_lo ? (sh.sel_lo + sh.sel_hi) / 2.0 : sh.sel_hi;
+            if (need_prev)
+                for (int w = 0; w < kSelWaves; ++w) lo_prev = fmax(lo_prev, sh.red2[w]);
+            cand_select(sh, cnt, kk, want_lo && !need_prev);
+            med = want_lo ? ((need_prev ? lo_prev : sh.sel_lo) + sh.sel_hi) / 2.0 : sh.sel_hi;
             K2_STAMP(10, cnt);
             __syncthreads();
         }
         K2_STAMP(6, clock64());
         if (mad_fast) {
-            for (uint32_t i = tid; i < ncand; i += kSelThreads) sh.cand[i] = fabs(res[sh.mcand[i]] - med);
+            for (uint32_t i = tid; i < ncand; i += kSelThreads) sh.cand[i] = fabs(res.r(sh.mcand[i]) - med);
             __syncthreads();
             cand_select(sh, ncand, kk2, want_lo);
             // the neighbour below the order statistic may be a counted (not gathered) slot unless it is >= L0
@@ -805,6 +890,7 @@ __global__ void __launch_bounds__(kSelThreads) align_scale_kernel(AlignArgs a, i
         }
         K2_STAMP(7, clock64());
         if (!mad_fast) {
+            if (!mat) materialize(res, M8);
             for (int i = tid; i < kBins; i += kSelThreads) sh.hist[i] = 0;
             __syncthreads();
             sweep_res(res, M8, [&](double r) { atomicAdd(&sh.hist[sel_bin<true>(fabs(r - med))], 1u); });
@@ -923,7 +1009,7 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
         return;
     }
     const PairDesc& P = a.pairs[pair];
-    const int nf = P.n_ref + P.n_kf, fstride = (nf + 7) & ~7;
+    const int nf = P.n_ref + P.n_kf;
     const int f = chunk * kLaneFeats + lane;
     const int W = a.geom.w[level];
     const int64_t loff = a.geom.off[level];
@@ -937,17 +1023,24 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
     if (fvis == 3) {
         const double pu = a.px[2 * gf], pv = a.px[2 * gf + 1];
         const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
-        const __amdgpu_buffer_rsrc_t rr = slot_rsrc(a.res + (int64_t)pair * a.res_stride, a.res_stride * 8);
-        const uint32_t fo = (uint32_t)f;
+        const double2 cp = reinterpret_cast<const double2*>(a.cproj)[gf];  // projection into cur (K1)
         const double ur = pu * scale, vr = pv * scale, fur = floor(ur), fvr = floor(vr);
         const double fx = ur - fur, gx = 1.0 - fx, fy = vr - fvr, gy = 1.0 - fy;
-        const int ru = (int)fur, rv = (int)fvr;
+        const double fcu = floor(cp.x), fcv = floor(cp.y);
+        const double cfx = cp.x - fcu, cgx = 1.0 - cfx, cfy = cp.y - fcv, cgy = 1.0 - cfy;
+        const int ru = (int)fur, rv = (int)fvr, qu = (int)fcu, qv = (int)fcv;
         const uint8_t* const plane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
-        uint32_t row[WB][NW];
+        const uint8_t* const cplane = P.cur_pyr + loff;
+        uint32_t row[WB][NW], crow[G::RB][G::RW];
 #pragma unroll
         for (int R = 0; R < WB; ++R) load_row<G::WD>(plane, (uint32_t)((rv - h - 1 + R) * W + (ru - h - 1)), row[R]);
+#pragma unroll
+        for (int r = 0; r < G::RB; ++r) load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
         double sxx = 0.0, sxy = 0.0, syy = 0.0, sxr = 0.0, syr = 0.0, chi = 0.0;
         double P3[side], P2[side], P1[side], P0[side], D2[side], D1[side], D0[side];  // P(R-3..R), D(R-2..R)
+        double cprev[side];  // cur row blends of patch row ky (window row ky)
+#pragma unroll
+        for (int kx = 0; kx < side; ++kx) cprev[kx] = fma(cfx, wbyte(crow[0], kx + 1), cgx * wbyte(crow[0], kx));
 #pragma unroll
         for (int R = 0; R < WB; ++R) {
             double hv[2 * h + 3];
@@ -965,7 +1058,11 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
                 const int ky = R - 3;
 #pragma unroll
                 for (int kx = 0; kx < side; ++kx) {
-                    const double r = slot_load(rr, 8 * fo, 8 * (uint32_t)((ky * side + kx) * fstride));
+                    const double ccur = fma(cfx, wbyte(crow[ky + 1], kx + 1), cgx * wbyte(crow[ky + 1], kx));
+                    const double I = fma(cfy, ccur, cgy * cprev[kx]);
+                    cprev[kx] = ccur;
+                    const double T = fma(fy, P1[kx], gy * P2[kx]);
+                    const double r = I - T;  // the residual of K1 up to rounding (shared weights)
                     const double dx = 0.5 * (gy * D2[kx] + fy * D1[kx]);
                     const double dy = 0.5 * (gy * (P1[kx] - P3[kx]) + fy * (P0[kx] - P2[kx]));
                     const double r2 = r * r;

@@ -68,14 +68,14 @@ struct svo_align_batch {
     svo_camera cam;
     svo_align_params params;
     int32_t n_pairs, max_f, half, area;
-    int64_t res_stride, key_stride;
+    int64_t key_stride;
     uint16_t* d_keys;
     svo::LevelGeom geom;
     std::vector<svo::PairDesc> h_pairs;
     std::vector<uint8_t> pair_set;
     svo::PairDesc* d_pairs;
     svo::PairState* d_state;
-    double *d_px, *d_bearing, *d_point, *d_xw, *d_partials, *d_res, *d_pose_out, *d_err;
+    double *d_px, *d_bearing, *d_point, *d_xw, *d_partials, *d_cproj, *d_scratch, *d_pose_out, *d_err;
     uint32_t* d_arrive;
     int32_t feat_iters, chunks;
     uint8_t *d_has_point, *d_fvis;
@@ -240,7 +240,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_keys,
-                    b->d_state, b->d_partials, b->d_arrive, b->d_fvis, b->d_res, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
+                    b->d_state, b->d_partials, b->d_arrive, b->d_fvis, b->d_cproj, b->d_scratch, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -282,10 +282,10 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_partials, (size_t)n_pairs * b->chunks * 28 * sizeof(double));
     ALLOC(b->d_arrive, (size_t)n_pairs * sizeof(uint32_t));
     ALLOC(b->d_fvis, F);
-    const int64_t slots = (int64_t)area * ((max_features + 7) / 8 * 8);  // pixel-major slots, see AlignArgs
-    b->res_stride = (slots + 63) / 64 * 64;
-    ALLOC(b->d_res, (size_t)n_pairs * b->res_stride * sizeof(double));
-    b->key_stride = b->res_stride;
+    const int64_t slots = (int64_t)area * ((max_features + 63) / 64 * 64);  // pixel-major slots, see AlignArgs
+    b->key_stride = slots;
+    ALLOC(b->d_cproj, F * 2 * sizeof(double));
+    ALLOC(b->d_scratch, (size_t)n_pairs * b->key_stride * sizeof(double));
     ALLOC(b->d_keys, (size_t)n_pairs * b->key_stride * sizeof(uint16_t));
     ALLOC(b->d_pose_out, (size_t)n_pairs * 7 * sizeof(double));
     ALLOC(b->d_err, (size_t)n_pairs * sizeof(double));
@@ -379,7 +379,7 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
     a.xw = b->d_xw; a.keys = b->d_keys; a.key_stride = b->key_stride; a.state = b->d_state; a.partials = b->d_partials;
     a.arrive = b->d_arrive;
-    a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.res = b->d_res; a.res_stride = b->res_stride;
+    a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.cproj = b->d_cproj; a.scratch = b->d_scratch;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
     a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
     a.min_level = b->params.min_level; a.max_level = b->params.max_level;

@@ -46,12 +46,13 @@ struct AlignArgs {
     double* partials;         // scratch [n_pairs][chunks][28] per-workgroup J^T W J (21) | J^T W r (6) | chi2
     uint32_t* arrive;         // scratch [n_pairs] K3 workgroups of the current level that have published partials
     // Residual slots of a pair are pixel-major: slot (k, f) = k * fstride + f for pixel k of the patch and
-    // feature f, fstride = n_features rounded up to 8 (one lane per feature reads and writes coalesced).
-    // Slots of features >= n_features are invisible.
-    double* res;              // scratch [n_pairs][res_stride] residual per pixel slot (+inf = invisible)
-    int64_t res_stride;       // >= area * round_up(max_f, 8), multiple of 64
+    // feature f, fstride = n_features rounded up to 64 (one lane per feature, one 128-B key line per wave
+    // and pixel).  Slots of features >= n_features are invisible.  Only the 16-bit keys are stored; exact
+    // residuals are recomputed from the images where needed (K2 candidates, K3).
+    double* cproj;            // scratch [n_pairs*max_f][2] projection (cu, cv) into the cur level (K1)
+    double* scratch;          // scratch [n_pairs][key_stride] exact residuals, written only by K2's exact paths
     uint16_t* keys;           // scratch [n_pairs][key_stride] 16-bit monotone key per slot (0xFFFF = invisible)
-    int64_t key_stride;       // >= area * round_up(max_f, 8), multiple of 64
+    int64_t key_stride;       // >= area * round_up(max_f, 64), multiple of 64
     double* pose_out;         // [n_pairs][7]
     double* err_out;          // [n_pairs]
     int32_t* status_out;      // [n_pairs]

@@ -53,8 +53,9 @@ def main():
         tot = np.median(s[:, 9] - s[:, 0])
         med_slow = int(np.sum(s[:, 10] >= 1000000))
         mad_slow = int(np.sum(s[:, 12] == 1))
-        print(f"level {level}: total={tot:.0f} cyc  {row}  | median cnt med={np.median(s[:, 10] % 1000000):.0f} "
-              f"slow={med_slow}  mad cand med={np.median(s[:, 11]):.0f} slow={mad_slow}")
+        print(f"level {level}: total={tot:.0f} cyc (max {np.max(s[:, 9] - s[:, 0]):.0f})  {row}  | median cnt "
+              f"med={np.median(s[:, 10] % 1000000):.0f} max={np.max(s[:, 10] % 1000000):.0f} slow={med_slow}  "
+              f"mad cand med={np.median(s[:, 11]):.0f} max={np.max(s[:, 11]):.0f} slow={mad_slow}")
 
 
 if __name__ == "__main__":
