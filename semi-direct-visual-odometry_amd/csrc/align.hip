@@ -31,7 +31,8 @@ namespace svo {
 
 namespace {
 
-constexpr int kLaneFeats = 64;       // K1 / K3 workgroup: one wave, one feature per lane
+constexpr int kLaneFeats = 256;      // K1 / K3 workgroup: 4 waves, one feature per lane
+constexpr int kLaneWaves = kLaneFeats / 64;
 constexpr int kSelThreads = 512;     // K2 workgroup (two per CU)
 constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kBins = 4096;
@@ -692,7 +693,8 @@ __device__ double block_median(SelShared& sh, const SlotSrc& res, int M, int Ms,
 __device__ uint64_t g_stamps[4096 * 16];
 #define K2_STAMP(i, v)                                                                      \
     do {                                                                                    \
-        if (tid == 0 && pair * 5 + level < 4096) g_stamps[(pair * 5 + level) * 16 + (i)] = (v); \
+        if (tid == 0 && (a.pair_base + pair) * 5 + level < 4096)                                \
+            g_stamps[((a.pair_base + pair) * 5 + level) * 16 + (i)] = (v);                      \
     } while (0)
 #else
 #define K2_STAMP(i, v) \
@@ -995,13 +997,15 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
     using G = Win<kHalf>;
     constexpr int h = G::h, side = G::side, WB = G::WB, NW = G::WW;
     __shared__ SolveShared ssh;
+    __shared__ double part[kLaneWaves][28];
+    __shared__ uint32_t last_flag;
     int pair, chunk;
     xcd_pair_chunk(a.chunks, pair, chunk);
     if (pair >= a.n_pairs) return;
     PairState& S = a.state[pair];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (!S.active) {  // nothing to align: the outputs are the initial state (K0)
-        if (level == a.min_level && chunk == 0 && lane == 0) {
+        if (level == a.min_level && chunk == 0 && tid == 0) {
             for (int i = 0; i < 7; ++i) a.pose_out[7 * pair + i] = S.pose[i];
             a.err_out[pair] = S.err;
             a.status_out[pair] = S.status;
@@ -1010,7 +1014,7 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
     }
     const PairDesc& P = a.pairs[pair];
     const int nf = P.n_ref + P.n_kf;
-    const int f = chunk * kLaneFeats + lane;
+    const int f = chunk * kLaneFeats + tid;
     const int W = a.geom.w[level];
     const int64_t loff = a.geom.off[level];
     const double dom = (double)(1 << level), scale = 1.0 / dom;
@@ -1105,19 +1109,28 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
         }
     }
     acc[0] += __shfl_xor(acc[0], 1, 64);
+    if ((lane & 1) == 0 && (lane >> 1) < 28) part[wave][lane >> 1] = acc[0];
+    __syncthreads();
     // publish (MI355X_MICROARCH.md, inter-workgroup visibility): the partials are stored write-through
-    // (agent-scope stores: sc1, they leave the XCD's L2), drained by the wave's vmcnt(0), then one lane adds
-    // to the pair's arrival counter; the workgroup whose add returns a.chunks - 1 is the last, acquires
-    // (invalidates its CU's L1) and takes the LM step.  No per-workgroup L2 write-back (release fence).
-    if ((lane & 1) == 0 && (lane >> 1) < 28)
-        __hip_atomic_store(a.partials + ((int64_t)pair * a.chunks + chunk) * 28 + (lane >> 1), acc[0], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t prev = 0;
-    if (lane == 0) prev = __hip_atomic_fetch_add(a.arrive + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    prev = __shfl(prev, 0, 64);
-    if (prev != (uint32_t)a.chunks - 1) return;
-    if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // (agent-scope stores: sc1, they leave the XCD's L2) by wave 0, drained by its vmcnt(0), then one lane
+    // adds to the pair's arrival counter; the workgroup whose add returns a.chunks - 1 is the last,
+    // acquires (invalidates its CU's L1) and takes the LM step.  No per-workgroup L2 write-back.
+    if (wave == 0) {
+        if (lane < 28) {
+            double t = 0.0;
+#pragma unroll
+            for (int w = 0; w < kLaneWaves; ++w) t += part[w][lane];
+            __hip_atomic_store(a.partials + ((int64_t)pair * a.chunks + chunk) * 28 + lane, t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            last_flag = __hip_atomic_fetch_add(a.arrive + pair, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (uint32_t)a.chunks - 1;
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     pair_step(a, S, level, pair, ssh);

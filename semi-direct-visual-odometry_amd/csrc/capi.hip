@@ -49,9 +49,14 @@ svo::LevelGeom make_geom(int32_t w, int32_t h, int32_t levels) {
 
 }  // namespace
 
+constexpr int32_t kSplitMin = 64;  // batches of at least this many pairs run as kSplits concurrent chains
+constexpr int kSplits = 2;         // measured on MI355X at 512 pairs: 1 / 2 / 3 / 4 chains = 335k / 355k / 359k / 352k pairs/s
+
 struct svo_ctx {
     int32_t device;
     hipStream_t stream;
+    hipStream_t sides[4];         // extra streams: a batch runs as concurrent sub-batch chains
+    hipEvent_t fork, joins[4];    // sides wait for stream at fork; stream waits for each side at its join
     hipEvent_t events[16];
 };
 
@@ -113,6 +118,9 @@ int svo_ctx_create(int32_t device, svo_ctx** out) {
     if (!c) return fail(SVO_ERR_ARG, "out of host memory");
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->sides[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->joins[i], hipEventDisableTiming);
     for (int i = 0; i < 16 && e == hipSuccess; ++i) e = hipEventCreate(&c->events[i]);
     if (e != hipSuccess) {
         delete c;
@@ -128,6 +136,11 @@ int svo_ctx_destroy(svo_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (hipEvent_t ev : c->events)
         if (ev) (void)hipEventDestroy(ev);
+    if (c->fork) (void)hipEventDestroy(c->fork);
+    for (int i = 1; i < 4; ++i) {
+        if (c->joins[i]) (void)hipEventDestroy(c->joins[i]);
+        if (c->sides[i]) (void)hipStreamDestroy(c->sides[i]);
+    }
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SVO_OK;
@@ -369,6 +382,22 @@ int svo_align_batch_set_initial_poses(svo_align_batch* b, const double* poses) {
     return SVO_OK;
 }
 
+// Pairs [p0, p0 + n) of a batch as a batch of their own (every per-pair array offset by p0).
+static svo::AlignArgs sub_batch(const svo::AlignArgs& a, const svo_align_batch* b, int32_t p0, int32_t n) {
+    svo::AlignArgs s = a;
+    const int64_t F = (int64_t)p0 * b->max_f;
+    s.pairs += p0; s.state += p0;
+    s.px += 2 * F; s.bearing += 3 * F; s.point += 3 * F; s.has_point += F; s.xw += 3 * F; s.fvis += F;
+    s.cproj += 2 * F;
+    s.partials += (int64_t)p0 * b->chunks * 28; s.arrive += p0;
+    s.keys += (int64_t)p0 * b->key_stride; s.scratch += (int64_t)p0 * b->key_stride;
+    s.pose_out += 7 * (int64_t)p0; s.err_out += p0; s.status_out += p0;
+    s.traces += (int64_t)p0 * (b->params.max_level + 1);
+    s.n_pairs = n;
+    s.pair_base = a.pair_base + p0;
+    return s;
+}
+
 static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     if (!b) return fail(SVO_ERR_ARG, "null argument");
     for (int32_t i = 0; i < b->n_pairs; ++i)
@@ -381,11 +410,30 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     a.arrive = b->d_arrive;
     a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.cproj = b->d_cproj; a.scratch = b->d_scratch;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
-    a.n_pairs = b->n_pairs; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
+    a.n_pairs = b->n_pairs; a.pair_base = 0; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
     a.min_level = b->params.min_level; a.max_level = b->params.max_level;
     a.fx = b->cam.fx; a.fy = b->cam.fy; a.cx = b->cam.cx; a.cy = b->cam.cy;
     a.geom = b->geom;
-    svo::launch_align(a, b->ctx->stream, marks);
+    svo_ctx* c = b->ctx;
+    if (marks || b->n_pairs < kSplitMin) {
+        svo::launch_align(a, c->stream, marks);
+    } else {
+        // two independent half-batch chains on two streams: one chain's latency-bound stages (the
+        // per-pair robust scale) overlap the other chain's feature stages.  Results are per pair and
+        // independent of the split.
+        const int ns = kSplits;
+        const int32_t per = (b->n_pairs / ns + 7) / 8 * 8;
+        SVO_HIP(hipEventRecord(c->fork, c->stream));
+        for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->fork, 0));
+        for (int i = 0; i < ns; ++i) {
+            const int32_t p0 = i * per, cnt = i == ns - 1 ? b->n_pairs - p0 : per;
+            svo::launch_align(sub_batch(a, b, p0, cnt), i == 0 ? c->stream : c->sides[i], nullptr);
+        }
+        for (int i = 1; i < ns; ++i) {
+            SVO_HIP(hipEventRecord(c->joins[i], c->sides[i]));
+            SVO_HIP(hipStreamWaitEvent(c->stream, c->joins[i], 0));
+        }
+    }
     SVO_HIP(hipGetLastError());
     b->ran = true;
     return SVO_OK;

@@ -58,6 +58,7 @@ struct AlignArgs {
     int32_t* status_out;      // [n_pairs]
     svo_level_trace* traces;  // [n_pairs][max_level+1]
     int32_t n_pairs, max_f, half, area, min_level, max_level;
+    int32_t pair_base;        // index of pair 0 of these arguments in the whole batch (sub-batch chains)
     int32_t feat_iters;       // feature groups one K1/K3 wave walks through
     int32_t chunks;           // K1/K3 workgroups per pair = align_chunks(max_f, half, feat_iters)
     double fx, fy, cx, cy;
