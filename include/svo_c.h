@@ -162,6 +162,47 @@ int svo_feature_align(svo_ctx* ctx, const svo_camera* cam, int32_t patch_size, c
                       const int32_t* ref_frames, int32_t ref_frame, const svo_pyramid_set* cur_set, int32_t cur_frame,
                       int32_t n, const double* ref_px, double* px_inout, double* err, int32_t* status);
 
+/* ---------------------------------------------------------------- depth filter
+ * One depth-filter seed: MixedGaussianFilter (include/mixed_gaussian_filter.hpp:28-38) and the feature
+ * it refines (m_feature: pixel position and bearing in its keyframe). */
+typedef struct {
+    double a, b, mu, sigma, var, max_depth; /* Beta(a, b) inlier ratio; inverse-depth N(mu, var); 1 / depthMin */
+    double px[2];                           /* m_feature->m_pixelPosition (keyframe, level 0) */
+    double bearing[3];                      /* m_feature->m_bearingVec */
+    int32_t kf;                             /* keyframe of m_feature->m_frame: index into the call's keyframe table */
+    int32_t valid;                          /* m_validity */
+} svo_depth_seed;
+
+/* Outcome of one seed in svo_depth_update (no reference counterpart; the reference only logs it). */
+enum {
+    SVO_DEPTH_REJECTED = 0,  /* point behind / outside the current image: seed invalid (src/depth_estimator.cpp:229-237) */
+    SVO_DEPTH_NO_MATCH = 1,  /* epipolar search failed: b += 1 (:252-258) */
+    SVO_DEPTH_UPDATED = 2,   /* Gaussian x Beta update (:261-266) */
+    SVO_DEPTH_CONVERGED = 3, /* sqrt(var) * 10 < max_depth: candidate point emitted, seed invalid (:281-291) */
+    SVO_DEPTH_NAN = 4        /* inverse depth NaN: seed invalid (:292-297) */
+};
+
+/* MixedGaussianFilter(feature, depthMean, depthMin) (src/mixed_gaussian_filter.cpp:7-24): initial state
+ * of a seed (px, bearing, kf are the caller's; valid = 1).  Host only. */
+int svo_depth_seed_init(double depth_mean, double depth_min, svo_depth_seed* seed);
+
+/* Replaces DepthEstimator::updateFilters(frame) (src/depth_estimator.cpp:192-309, with
+ * algorithm::matchEpipolarConstraint src/algorithm.cpp:412-551, computeTau :342-357, updateFilter
+ * :311-340): every seed against the current frame, then the reference's stable remove_if of invalid
+ * seeds.  Keyframe k of the table is frame kf_frames[k] of kf_sets[k] (its level-0 intensity image) with
+ * pose kf_poses[7k..7k+6]; the current frame is cur_frame of cur_set with pose cur_pose (Sophus params).
+ *   seeds_inout   n_seeds in; the n_seeds_out survivors out (order kept)
+ *   outcome       n_seeds (per input seed, SVO_DEPTH_*), may be NULL
+ *   cand_points   n_seeds x 3 capacity: world points of the converged seeds (m_map->addNewCandidate),
+ *   cand_seed     n_seeds capacity: their input seed index; both in the reference's loop order
+ *                 (seeds visited from the last to the first); *n_cand entries.
+ * Synchronous. */
+int svo_depth_update(svo_ctx* ctx, const svo_camera* cam, int32_t n_kf, const svo_pyramid_set* const* kf_sets,
+                     const int32_t* kf_frames, const double* kf_poses, const svo_pyramid_set* cur_set,
+                     int32_t cur_frame, const double* cur_pose, int32_t n_seeds, svo_depth_seed* seeds_inout,
+                     int32_t* n_seeds_out, int32_t* outcome, double* cand_points, int32_t* cand_seed,
+                     int32_t* n_cand);
+
 #ifdef __cplusplus
 }
 #endif

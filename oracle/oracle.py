@@ -208,3 +208,60 @@ def feature_align(cam, patch, ref_grad, cur_grad, ref_px, px_init):
     lib().oracle_feature_align(ctypes.byref(camera(cam)), patch, _p(ref_grad), _p(cur_grad), n, _p(ref_px), _p(px),
                                _p(err), _p(st))
     return px, err, st
+
+
+# ---------------------------------------------------------------- depth filter (config 5)
+DEPTH_SEED = np.dtype([("a", "f8"), ("b", "f8"), ("mu", "f8"), ("sigma", "f8"), ("var", "f8"), ("max_depth", "f8"),
+                       ("px", "f8", 2), ("bearing", "f8", 3), ("kf", "i4"), ("valid", "i4")])
+
+
+def depth_seed_init(depth_mean, depth_min):
+    """MixedGaussianFilter(feature, depthMean, depthMin): (a, b, mu, sigma, var, max_depth)."""
+    out = np.zeros(6)
+    lib().oracle_depth_seed_init(ctypes.c_double(depth_mean), ctypes.c_double(depth_min), _p(out))
+    return out
+
+
+def make_seeds(px, bearing, depth_mean, depth_min, kf=0):
+    """Seeds for features (px, bearing) of keyframe `kf` (DepthEstimator::initializeFilters)."""
+    n = len(px)
+    s = np.zeros(n, DEPTH_SEED)
+    a, b, mu, sigma, var, md = depth_seed_init(depth_mean, depth_min)
+    s["a"], s["b"], s["mu"], s["sigma"], s["var"], s["max_depth"] = a, b, mu, sigma, var, md
+    s["px"], s["bearing"], s["kf"], s["valid"] = px, bearing, kf, 1
+    return s
+
+
+def depth_update(cam, kf_imgs, kf_poses, cur_img, cur_pose, seeds):
+    """DepthEstimator::updateFilters.  Returns (survivors, outcome[n], cand_points[m,3], cand_seed[m])."""
+    assert lib().oracle_depth_seed_size() == DEPTH_SEED.itemsize
+    seeds = np.ascontiguousarray(seeds, DEPTH_SEED).copy()
+    n = len(seeds)
+    imgs = [np.ascontiguousarray(i, np.uint8) for i in kf_imgs]
+    ptrs = (ctypes.c_void_p * max(len(imgs), 1))(*[_p(i).value for i in imgs])
+    kp = np.ascontiguousarray(kf_poses, np.float64).reshape(-1, 7)
+    cur = np.ascontiguousarray(cur_img, np.uint8)
+    cp = np.ascontiguousarray(cur_pose, np.float64)
+    outc = np.zeros(n, np.int32)
+    pts = np.zeros((max(n, 1), 3))
+    cs = np.zeros(max(n, 1), np.int32)
+    n_out, n_cand = ctypes.c_int32(), ctypes.c_int32()
+    lib().oracle_depth_update(ctypes.byref(camera(cam)), len(imgs), ptrs, _p(kp), _p(cur), _p(cp), n, _p(seeds),
+                              ctypes.byref(n_out), _p(outc), _p(pts), _p(cs), ctypes.byref(n_cand))
+    return seeds[:n_out.value].copy(), outc, pts[:n_cand.value].copy(), cs[:n_cand.value].copy()
+
+
+def zsad(ref, cur):
+    ref = np.ascontiguousarray(ref, np.uint8)
+    cur = np.ascontiguousarray(cur, np.uint8)
+    L = lib()
+    L.oracle_zsad.restype = ctypes.c_double
+    return L.oracle_zsad(_p(ref), _p(cur), len(ref))
+
+
+def depth_triangulate(rel_pose, f_ref, f_cur):
+    """(ok, depth) of algorithm::depthFromTriangulation."""
+    d = ctypes.c_double()
+    r, a, b = (np.ascontiguousarray(x, np.float64) for x in (rel_pose, f_ref, f_cur))
+    ok = lib().oracle_depth_triangulate(_p(r), _p(a), _p(b), ctypes.byref(d))
+    return bool(ok), d.value

@@ -686,6 +686,191 @@ struct FeatureAlignment {
     }
 };
 
+// ------------------------------------------------------------------ depth filter (config 5)
+// DepthEstimator::updateFilters (src/depth_estimator.cpp:192-309) with its helpers.  Seeds are the
+// MixedGaussianFilter state (include/mixed_gaussian_filter.hpp:28-38) plus the feature they refine.
+struct DepthSeed {
+    double a, b, mu, sigma, var, max_depth;
+    double px[2];
+    double bearing[3];
+    int32_t kf, valid;
+};
+enum DepthOutcome : int32_t {  // per seed, for the parity tests (no reference counterpart)
+    kDepthRejected = 0,        // pointInCurCamera.z < 0 or outside the cur image (:229-237): invalid
+    kDepthNoMatch = 1,         // matchEpipolarConstraint failed: b += 1 (:252-258)
+    kDepthUpdated = 2,         // Vogiatzis update, still a seed (:261-266)
+    kDepthConverged = 3,       // sqrt(var) * 10 < maxDepth: candidate point emitted, seed invalid (:281-291)
+    kDepthNaN = 4              // inverse depth NaN (:292-297): invalid
+};
+
+// Frame::image2camera (src/frame.cpp:104-107): inverseProject2d(px) * depth
+static V3 image2camera(const Camera& cam, V2 px, double depth) { return scl(cam.inverse_project2d(px.x, px.y), depth); }
+// algorithm::computeRelativePose (src/algorithm.cpp:705-709): T_cur * T_ref^-1
+static SE3 relative_pose(const SE3& ref, const SE3& cur) { return compose(cur, inverse(ref)); }
+
+// algorithm::getAffineWarp (src/algorithm.cpp:335-367); A row-major: A[0] = (0,0), A[1] = (0,1) ...
+static void affine_warp(const Camera& cam, const SE3& rel, V2 px, uint32_t patch, double depth, double A[4]) {
+    const uint32_t half = patch / 2;
+    const V3 c = image2camera(cam, px, depth);
+    const V3 du = image2camera(cam, {px.x + (double)half, px.y + 0.0}, depth);
+    const V3 dv = image2camera(cam, {px.x + 0.0, px.y + (double)half}, depth);
+    const V2 cc = cam.project2d(act(rel, c)), uc = cam.project2d(act(rel, du)), vc = cam.project2d(act(rel, dv));
+    A[0] = (uc.x - cc.x) / (double)half; A[2] = (uc.y - cc.y) / (double)half;  // column 0 = duDiff / h
+    A[1] = (vc.x - cc.x) / (double)half; A[3] = (vc.y - cc.y) / (double)half;  // column 1 = dvDiff / h
+}
+// algorithm::applyAffineWarp (src/algorithm.cpp:369-394): samples only if the location is inside the
+// frame by ceil(max |A (h, h)|) + 2 px; otherwise `data` keeps its previous contents
+static void apply_affine_warp(const Camera& cam, const Image& im, V2 loc, int32_t half, const double A[4], uint8_t* data) {
+    const double bx = A[0] * half + A[1] * half, by = A[2] * half + A[3] * half;
+    const double maxb = std::ceil(std::max(std::fabs(bx), std::fabs(by))) + 2;
+    if (!cam.is_in_frame(loc, maxb)) return;
+    uint32_t idx = 0;
+    for (int32_t i = -half; i <= half; ++i)
+        for (int32_t j = -half; j <= half; ++j) {
+            const double x = loc.x + (A[0] * j + A[1] * i), y = loc.y + (A[2] * j + A[3] * i);
+            data[idx++] = (uint8_t)bilinear_f(im, x, y);
+        }
+}
+// algorithm::computeScore (src/algorithm.cpp:396-410): ZSAD with Eigen's uint8 mean (sum wraps mod 256,
+// then uint8 / uint8)
+static double compute_score(const uint8_t* ref, const uint8_t* cur, int n) {
+    uint8_t sr = 0, sc = 0;
+    for (int i = 0; i < n; ++i) { sr = (uint8_t)(sr + ref[i]); sc = (uint8_t)(sc + cur[i]); }
+    const double mr = (double)(uint8_t)(sr / (uint8_t)n), mc = (double)(uint8_t)(sc / (uint8_t)n);
+    double sum = 0.0;
+    for (int i = 0; i < n; ++i) sum += std::fabs((ref[i] - mr) - (cur[i] - mc));
+    return sum;
+}
+// algorithm::depthFromTriangulation (src/algorithm.cpp:682-703), Eigen evaluation order
+static bool depth_from_triangulation(const SE3& rel, V3 fr, V3 fc, double& depth) {
+    double R[3][3];
+    rotmat(rel.q, R);
+    const V3 rf{R[0][0] * fr.x + R[0][1] * fr.y + R[0][2] * fr.z, R[1][0] * fr.x + R[1][1] * fr.y + R[1][2] * fr.z,
+                R[2][0] * fr.x + R[2][1] * fr.y + R[2][2] * fr.z};
+    const double A[3][2] = {{rf.x, -fc.x}, {rf.y, -fc.y}, {rf.z, -fc.z}};
+    double M[2][2];
+    for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) M[i][j] = A[0][i] * A[0][j] + A[1][i] * A[1][j] + A[2][i] * A[2][j];
+    const double det = M[0][0] * M[1][1] - M[1][0] * M[0][1];
+    if (det < 0.000001) return false;
+    const double invdet = 1.0 / det;
+    const double Inv[2][2] = {{M[1][1] * invdet, -M[0][1] * invdet}, {-M[1][0] * invdet, M[0][0] * invdet}};
+    const double t[3] = {rel.t.x, rel.t.y, rel.t.z};
+    double tmp[2][3];  // (-Inv) * A^T
+    for (int i = 0; i < 2; ++i)
+        for (int k = 0; k < 3; ++k) tmp[i][k] = (-Inv[i][0]) * A[k][0] + (-Inv[i][1]) * A[k][1];
+    const double d0 = tmp[0][0] * t[0] + tmp[0][1] * t[1] + tmp[0][2] * t[2];
+    depth = std::fabs(d0);
+    return true;
+}
+static V2 clamp_to_image(V2 p, const Camera& cam) {  // src/algorithm.cpp:435-450
+    p.x = p.x >= 0 ? p.x : 0.0;
+    p.x = p.x < cam.width ? p.x : cam.width - 1;
+    p.y = p.y >= 0 ? p.y : 0.0;
+    p.y = p.y < cam.height ? p.y : cam.height - 1;
+    return p;
+}
+// algorithm::matchEpipolarConstraint (src/algorithm.cpp:412-551) on the base (level-0) intensity images
+static bool match_epipolar(const Camera& cam, const Image& ref_im, const SE3& ref_pose, const Image& cur_im,
+                           const SE3& cur_pose, V2 px, V3 bearing, uint32_t patch, double d0, double dmin, double dmax,
+                           double& depth) {
+    const uint32_t half = patch / 2, area = patch * patch;
+    const SE3 rel = relative_pose(ref_pose, cur_pose);
+    const uint32_t thr = area * 128;
+    V2 lc = cam.project2d(act(rel, image2camera(cam, px, d0)));
+    V2 lmin = cam.project2d(act(rel, image2camera(cam, px, dmin)));
+    V2 lmax = cam.project2d(act(rel, image2camera(cam, px, dmax)));
+    lc = clamp_to_image(lc, cam);
+    lmin = clamp_to_image(lmin, cam);
+    lmax = clamp_to_image(lmax, cam);
+    const V2 epi{lmax.x - lmin.x, lmax.y - lmin.y};
+    double A[4];
+    affine_warp(cam, rel, px, patch, d0, A);
+    const double norm_epi = std::sqrt(epi.x * epi.x + epi.y * epi.y);
+    std::vector<uint8_t> refp(area, 0), curp(area, 0);
+    const double I[4] = {1.0, 0.0, 0.0, 1.0};
+    apply_affine_warp(cam, ref_im, px, (int32_t)half, I, refp.data());
+    if (norm_epi < 2.0) {
+        const V2 center{(lmax.x + lmin.x) / 2.0, (lmax.y + lmin.y) / 2.0};
+        return depth_from_triangulation(rel, bearing, cam.inverse_project2d(center.x, center.y), depth);
+    }
+    const uint32_t steps = (uint32_t)std::ceil(norm_epi);
+    const V2 step{epi.x / norm_epi, epi.y / norm_epi};
+    double best = std::numeric_limits<double>::max();
+    V2 best_loc{0.0, 0.0};
+    for (uint32_t i = 0; i < steps; ++i) {
+        const V2 loc{lmin.x + i * step.x, lmin.y + i * step.y};
+        apply_affine_warp(cam, cur_im, loc, (int32_t)half, A, curp.data());
+        const double z = compute_score(refp.data(), curp.data(), (int)area);
+        if (z < best) { best = z; best_loc = loc; }
+    }
+    if (best < thr) return depth_from_triangulation(rel, bearing, cam.inverse_project2d(best_loc.x, best_loc.y), depth);
+    return false;
+}
+// DepthEstimator::computeTau (src/depth_estimator.cpp:342-357)
+static double compute_tau(const SE3& rel, V3 f, double depth, double err_angle) {
+    const V3 t = rel.t;
+    const V3 diff = sub(scl(f, depth), t);
+    const double nt = norm(t), nd = norm(diff);
+    const double alpha = std::acos(dot(f, t) / nt);
+    const double beta = std::acos(dot(diff, scl(t, -1.0)) / (nt * nd));
+    const double beta_u = beta + err_angle;
+    const double gamma_u = 3.141592653589793 - alpha - beta_u;
+    const double depth_u = nt * std::sin(beta_u) / std::sin(gamma_u);
+    return depth_u - depth;
+}
+// DepthEstimator::updateFilter (src/depth_estimator.cpp:311-340) + computeNormalDistribution
+// (src/algorithm.cpp:907-911)
+static void update_filter(double x, double tau2, DepthSeed& s) {
+    const double norm_scale = std::sqrt(s.var + tau2);
+    if (std::isnan(norm_scale)) return;
+    const double s2 = 1.0 / (1.0 / s.var + 1.0 / tau2);
+    const double m = s2 * (s.mu / s.var + x / tau2);
+    const double p = (x - s.mu) / norm_scale;
+    const double nd = 0.3989422804014327 / norm_scale * std::exp(-0.5 * p * p);
+    double C1 = s.a / (s.a + s.b) * nd;
+    double C2 = s.b / (s.a + s.b) * 1.00 / s.max_depth;
+    const double nc = C1 + C2;
+    C1 /= nc;
+    C2 /= nc;
+    const double f = C1 * (s.a + 1.0) / (s.a + s.b + 1.0) + C2 * s.a / (s.a + s.b + 1.0);
+    const double e = C1 * (s.a + 1.0) * (s.a + 2.0) / ((s.a + s.b + 1.0) * (s.a + s.b + 2.0)) +
+                     C2 * s.a * (s.a + 1.0) / ((s.a + s.b + 1.0) * (s.a + s.b + 2.0));
+    const double new_mu = C1 * m + C2 * s.mu;
+    s.var = C1 * (s2 + m * m) + C2 * (s.var + s.mu * s.mu) - new_mu * new_mu;
+    s.sigma = std::sqrt(s.var);
+    s.mu = new_mu;
+    s.a = (e - f) / (f - e / f);
+    s.b = s.a * (1.0 - f) / f;
+}
+// one seed of DepthEstimator::updateFilters (:213-297); returns the outcome, `point` for a candidate
+static int32_t update_seed(const Camera& cam, const Image& kf_im, const SE3& kf_pose, const Image& cur_im,
+                           const SE3& cur_pose, double err_angle, DepthSeed& s, V3& point) {
+    const SE3 rel = relative_pose(kf_pose, cur_pose);
+    const V3 f{s.bearing[0], s.bearing[1], s.bearing[2]};
+    const V3 pc = act(rel, V3{f.x / s.mu, f.y / s.mu, f.z / s.mu});
+    if (pc.z < 0 || !cam.is_in_frame(cam.project2d(pc), 0.0)) { s.valid = 0; return kDepthRejected; }
+    const double inv_min = s.mu + s.var;
+    const double inv_max = std::max(s.mu - s.var, 1e-7);
+    double depth = 0.0;
+    if (!match_epipolar(cam, kf_im, kf_pose, cur_im, cur_pose, {s.px[0], s.px[1]}, f, 7, 1.0 / s.mu, 1.0 / inv_min,
+                        1.0 / inv_max, depth)) {
+        s.b++;
+        return kDepthNoMatch;
+    }
+    const double tau = compute_tau(rel, f, depth, err_angle);
+    const double inv_tau = 0.5 * (1.0 / std::max(1e-7, depth - tau) - 1.0 / (depth + tau));
+    update_filter(1.0 / depth, inv_tau * inv_tau, s);
+    if (std::sqrt(s.var) * 10.0 < s.max_depth) {
+        const V3 pcam = image2camera(cam, {s.px[0], s.px[1]}, 1.0 / s.mu);  // Frame::image2world (:109-113)
+        point = act(inverse(kf_pose), pcam);
+        s.valid = 0;
+        return kDepthConverged;
+    }
+    if (std::isnan(inv_min)) { s.valid = 0; return kDepthNaN; }
+    return kDepthUpdated;
+}
+
 }  // namespace oracle
 
 // =====================================================================================================
@@ -834,6 +1019,57 @@ void oracle_feature_align(const oc_camera* c, int32_t patch, const uint8_t* ref_
         px_inout[2 * i + 1] = px.y;
         if (status_out) status_out[i] = st;
     }
+}
+
+// MixedGaussianFilter::MixedGaussianFilter (src/mixed_gaussian_filter.cpp:7-24)
+void oracle_depth_seed_init(double depth_mean, double depth_min, double* a_b_mu_sigma_var_maxdepth) {
+    double* o = a_b_mu_sigma_var_maxdepth;
+    o[0] = 10; o[1] = 10; o[2] = 1.0 / depth_mean; o[5] = 1.0 / depth_min;
+    o[3] = o[5] / 6; o[4] = o[3] * o[3];
+}
+
+// DepthEstimator::updateFilters (src/depth_estimator.cpp:192-309) for n seeds against one cur frame.
+// kf_imgs[k] / kf_poses[7k]: level-0 intensity image and pose of keyframe k (seed.kf indexes them).
+// seeds (n, in/out): updated in place, then compacted like the reference's remove_if (stable) to
+// *n_out survivors.  outcome[n]: per input seed (DepthOutcome).  Candidates (m_map->addNewCandidate, in
+// the reverse seed order of the update loop): cand_points[3 * c], cand_seed[c] (input index), *n_cand.
+void oracle_depth_update(const oc_camera* c, int32_t n_kf, const uint8_t* const* kf_imgs, const double* kf_poses,
+                         const uint8_t* cur_img, const double* cur_pose, int32_t n, void* seeds_v, int32_t* n_out,
+                         int32_t* outcome, double* cand_points, int32_t* cand_seed, int32_t* n_cand) {
+    (void)n_kf;
+    Camera cam{c->fx, c->fy, c->cx, c->cy, c->width, c->height};
+    DepthSeed* seeds = (DepthSeed*)seeds_v;
+    auto pose = [](const double* p) { return SE3{{p[0], p[1], p[2], p[3]}, {p[4], p[5], p[6]}}; };
+    const SE3 cp = pose(cur_pose);
+    const Image ci{cur_img, c->width, c->height};
+    const double err_angle = std::atan(1.0 / (2.0 * c->fx)) * 2.0;  // :202-206 (pixel noise 1)
+    int32_t nc = 0;
+    for (int32_t i = n - 1; i >= 0; --i) {
+        DepthSeed& s = seeds[i];
+        const Image ki{kf_imgs[s.kf], c->width, c->height};
+        V3 pt{0, 0, 0};
+        outcome[i] = update_seed(cam, ki, pose(kf_poses + 7 * s.kf), ci, cp, err_angle, s, pt);
+        if (outcome[i] == kDepthConverged) {
+            cand_points[3 * nc] = pt.x; cand_points[3 * nc + 1] = pt.y; cand_points[3 * nc + 2] = pt.z;
+            cand_seed[nc++] = i;
+        }
+    }
+    int32_t k = 0;
+    for (int32_t i = 0; i < n; ++i)
+        if (seeds[i].valid) seeds[k++] = seeds[i];
+    *n_out = k;
+    *n_cand = nc;
+}
+
+int32_t oracle_depth_seed_size(void) { return (int32_t)sizeof(DepthSeed); }
+
+// algorithm::computeScore (src/algorithm.cpp:396-410) on two n-byte patches
+double oracle_zsad(const uint8_t* ref, const uint8_t* cur, int32_t n) { return compute_score(ref, cur, n); }
+
+// algorithm::depthFromTriangulation (src/algorithm.cpp:682-703); returns 0 when rejected (det < 1e-6)
+int32_t oracle_depth_triangulate(const double* rel7, const double* fref, const double* fcur, double* depth) {
+    const SE3 rel{{rel7[0], rel7[1], rel7[2], rel7[3]}, {rel7[4], rel7[5], rel7[6]}};
+    return depth_from_triangulation(rel, {fref[0], fref[1], fref[2]}, {fcur[0], fcur[1], fcur[2]}, *depth) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -29,6 +29,15 @@ class SvoAlignParams(ctypes.Structure):
     _fields_ = [("patch_size", c_int32), ("min_level", c_int32), ("max_level", c_int32), ("median_mode", c_int32)]
 
 
+class SvoDepthSeed(ctypes.Structure):
+    _fields_ = [("a", c_double), ("b", c_double), ("mu", c_double), ("sigma", c_double), ("var", c_double),
+                ("max_depth", c_double), ("px", c_double * 2), ("bearing", c_double * 3), ("kf", c_int32),
+                ("valid", c_int32)]
+
+
+DEPTH_OUTCOMES = {0: "Rejected", 1: "No_Match", 2: "Updated", 3: "Converged", 4: "NaN"}
+
+
 class SvoLevelTrace(ctypes.Structure):
     _fields_ = [("level", c_int32), ("n_ref_vis", c_int32), ("n_vis", c_int32), ("status", c_int32),
                 ("median", c_double), ("mad", c_double), ("sigma", c_double), ("chi2", c_double),
@@ -67,6 +76,10 @@ _SIGNATURES = [
     ("svo_align_batch_traces", c_int32, [c_void_p, c_int32, c_void_p]),
     ("svo_feature_align", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_int32,
                                     c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("svo_depth_seed_init", c_int32, [c_double, c_double, c_void_p]),
+    ("svo_depth_update", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_int32, c_void_p, c_int32, c_void_p, P_i32, c_void_p, c_void_p,
+                                   c_void_p, P_i32]),
 ]
 
 EXPORTED = [s[0] for s in _SIGNATURES]

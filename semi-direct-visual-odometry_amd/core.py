@@ -377,3 +377,84 @@ class FeatureAlignment:
         check(lib().svo_feature_align(self.ctx.handle, ctypes.byref(cam), self.patch_size, ref_set.handle, ptr(rf), 0,
                                       cur_set.handle, int(cur_frame), n, ptr(ref_px), ptr(px_inout), ptr(err), ptr(st)))
         return err, st
+
+
+# ---------------------------------------------------------------- depth filter
+DEPTH_SEED = np.dtype([("a", "f8"), ("b", "f8"), ("mu", "f8"), ("sigma", "f8"), ("var", "f8"), ("max_depth", "f8"),
+                       ("px", "f8", 2), ("bearing", "f8", 3), ("kf", "i4"), ("valid", "i4")])  # svo_depth_seed
+
+
+def depth_seeds(px, bearing, depth_mean, depth_min, kf=0):
+    """MixedGaussianFilter(feature, depthMean, depthMin) for each feature (src/mixed_gaussian_filter.cpp:7-24)."""
+    n = len(px)
+    s = np.zeros(n, DEPTH_SEED)
+    one = _capi.SvoDepthSeed()
+    check(lib().svo_depth_seed_init(float(depth_mean), float(depth_min), ctypes.byref(one)))
+    for k in ("a", "b", "mu", "sigma", "var", "max_depth"):
+        s[k] = getattr(one, k)
+    s["px"], s["bearing"], s["kf"], s["valid"] = px, bearing, kf, 1
+    return s
+
+
+def depth_update(camera, keyframes, cur, cur_pose, seeds, ctx=None):
+    """DepthEstimator::updateFilters for `seeds` (DEPTH_SEED array) against the current frame.
+
+    keyframes: list of (PyramidSet, frame index, pose[7]); seed["kf"] indexes it.  cur: (PyramidSet, frame).
+    Returns (survivors, outcome[n], cand_points[m, 3], cand_seed[m]) in the reference's orders."""
+    ctx = ctx or default_context()
+    seeds = np.ascontiguousarray(seeds, DEPTH_SEED).copy()
+    n = len(seeds)
+    nk = len(keyframes)
+    sets = (ctypes.c_void_p * max(nk, 1))(*[k[0].handle.value for k in keyframes])
+    frames = np.array([k[1] for k in keyframes] or [0], np.int32)
+    poses = np.ascontiguousarray(np.array([k[2] for k in keyframes] or [np.zeros(7)], np.float64))
+    cp = np.ascontiguousarray(cur_pose, np.float64)
+    outcome = np.zeros(max(n, 1), np.int32)
+    pts = np.zeros((max(n, 1), 3))
+    cs = np.zeros(max(n, 1), np.int32)
+    n_out, n_cand = ctypes.c_int32(), ctypes.c_int32()
+    cam = camera.as_c()
+    check(lib().svo_depth_update(ctx.handle, ctypes.byref(cam), nk, ctypes.cast(sets, ctypes.c_void_p), ptr(frames),
+                                 ptr(poses), cur[0].handle, int(cur[1]), ptr(cp), n, ptr(seeds), ctypes.byref(n_out),
+                                 ptr(outcome), ptr(pts), ptr(cs), ctypes.byref(n_cand)))
+    return seeds[:n_out.value].copy(), outcome[:n], pts[:n_cand.value].copy(), cs[:n_cand.value].copy()
+
+
+class DepthEstimator:
+    """DepthEstimator (include/depth_estimator.hpp, src/depth_estimator.cpp) without its worker thread:
+    add_keyframe = initializeFilters (:175-190) for the keyframe's features without a point,
+    update_filters = updateFilters (:192-309).  Converged seeds become candidates (Map::addNewCandidate,
+    src/map.cpp:586-593): (feature, Point) pairs in the reference's order."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx or default_context()
+        self.keyframes = []   # Frame objects; seed["kf"] indexes this list
+        self.features = []    # the Feature behind every seed, same order as self.seeds
+        self.seeds = np.zeros(0, DEPTH_SEED)
+        self.candidates = []
+
+    def add_keyframe(self, frame, depth_mean, depth_min):
+        feats = [f for f in frame.features if f.point is None]
+        kf = len(self.keyframes)
+        self.keyframes.append(frame)
+        if feats:
+            px = np.array([f.pixel_position for f in feats])
+            br = np.array([f.bearing_vec for f in feats])
+            self.seeds = np.concatenate([self.seeds, depth_seeds(px, br, depth_mean, depth_min, kf)])
+            self.features += feats
+
+    def number_filters(self):
+        return len(self.seeds)
+
+    def update_filters(self, frame):
+        if len(self.seeds) == 0:
+            return []
+        kfs = [(k.image_pyramid.set, 0, k.abs_pose) for k in self.keyframes]
+        surv, outcome, pts, cs = depth_update(frame.camera, kfs, (frame.image_pyramid.set, 0), frame.abs_pose,
+                                              self.seeds, self.ctx)
+        new = [(self.features[i], Point(p)) for i, p in zip(cs, pts)]
+        self.candidates += new
+        keep = [i for i in range(len(self.seeds)) if outcome[i] in (1, 2) and self.seeds[i]["valid"]]  # still seeds
+        self.features = [self.features[i] for i in keep]
+        self.seeds = surv
+        return new

@@ -1,6 +1,7 @@
 // capi.hip — the C ABI (include/svo_c.h): contexts, device-resident pyramid sets, alignment batches.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -545,6 +546,99 @@ int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, con
     for (void* p : {(void*)d_rg, (void*)d_st, (void*)d_rpx, (void*)d_px, (void*)d_err})
         if (p) (void)hipFree(p);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ depth filter
+int svo_depth_seed_init(double depth_mean, double depth_min, svo_depth_seed* seed) {
+    if (!seed) return fail(SVO_ERR_ARG, "null seed");
+    seed->a = 10;                          // src/mixed_gaussian_filter.cpp:10-11
+    seed->b = 10;
+    seed->mu = 1.0 / depth_mean;           // :13
+    seed->max_depth = 1.0 / depth_min;     // :14
+    seed->sigma = seed->max_depth / 6;     // :18
+    seed->var = seed->sigma * seed->sigma; // :20
+    seed->valid = 1;                       // :21
+    return SVO_OK;
+}
+
+int svo_depth_update(svo_ctx* c, const svo_camera* cam, int32_t n_kf, const svo_pyramid_set* const* kf_sets,
+                     const int32_t* kf_frames, const double* kf_poses, const svo_pyramid_set* cur_set,
+                     int32_t cur_frame, const double* cur_pose, int32_t n, svo_depth_seed* seeds,
+                     int32_t* n_out, int32_t* outcome, double* cand_points, int32_t* cand_seed, int32_t* n_cand) {
+    if (!c || !cam || !cur_set || !cur_pose || !n_out || !n_cand || (n_kf > 0 && (!kf_sets || !kf_frames || !kf_poses)))
+        return fail(SVO_ERR_ARG, "null argument");
+    if (n < 0 || n_kf < 0) return fail(SVO_ERR_ARG, "negative count");
+    if (n > 0 && (!seeds || !cand_points || !cand_seed)) return fail(SVO_ERR_ARG, "null seed / candidate array");
+    auto check_set = [&](const svo_pyramid_set* p, int32_t frame) -> int {
+        if (!p) return fail(SVO_ERR_ARG, "null pyramid set");
+        if (p->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
+        if (p->width != cam->width || p->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
+        if (frame < 0 || frame >= p->n_frames) return fail(SVO_ERR_ARG, "frame %d out of range", frame);
+        return SVO_OK;
+    };
+    int rc;
+    if ((rc = check_set(cur_set, cur_frame)) != SVO_OK) return rc;
+    std::vector<const uint8_t*> kimg(n_kf > 0 ? n_kf : 1);
+    for (int32_t k = 0; k < n_kf; ++k) {
+        if ((rc = check_set(kf_sets[k], kf_frames[k])) != SVO_OK) return rc;
+        kimg[k] = kf_sets[k]->d_base + (size_t)kf_frames[k] * kf_sets[k]->stride;  // intensity stack, level 0
+    }
+    for (int32_t i = 0; i < n; ++i)
+        if (seeds[i].kf < 0 || seeds[i].kf >= n_kf) return fail(SVO_ERR_ARG, "seed %d: keyframe %d out of range", i, seeds[i].kf);
+    *n_out = 0;
+    *n_cand = 0;
+    if (n == 0) return SVO_OK;
+    SVO_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    svo::DepthArgs a{};
+    svo_depth_seed *d_seeds = nullptr, *d_new = nullptr, *d_out = nullptr;
+    int32_t *d_outc = nullptr, *d_cseed = nullptr, *d_counts = nullptr;
+    double *d_points = nullptr, *d_cpts = nullptr, *d_kpose = nullptr, *d_cpose = nullptr;
+    const uint8_t** d_kimg = nullptr;
+    hipError_t e = hipSuccess;
+#define DALLOC(ptr, bytes) if (e == hipSuccess) e = hipMalloc(&ptr, bytes)
+    DALLOC(d_seeds, n * sizeof(svo_depth_seed));
+    DALLOC(d_new, n * sizeof(svo_depth_seed));
+    DALLOC(d_out, n * sizeof(svo_depth_seed));
+    DALLOC(d_outc, n * sizeof(int32_t));
+    DALLOC(d_cseed, n * sizeof(int32_t));
+    DALLOC(d_counts, 2 * sizeof(int32_t));
+    DALLOC(d_points, n * 3 * sizeof(double));
+    DALLOC(d_cpts, n * 3 * sizeof(double));
+    DALLOC(d_kpose, (size_t)(n_kf > 0 ? n_kf : 1) * 7 * sizeof(double));
+    DALLOC(d_cpose, 7 * sizeof(double));
+    DALLOC(d_kimg, (size_t)(n_kf > 0 ? n_kf : 1) * sizeof(void*));
+#undef DALLOC
+    if (e == hipSuccess) e = hipMemcpyAsync(d_seeds, seeds, n * sizeof(svo_depth_seed), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && n_kf > 0) e = hipMemcpyAsync(d_kpose, kf_poses, n_kf * 7 * sizeof(double), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && n_kf > 0) e = hipMemcpyAsync(d_kimg, kimg.data(), n_kf * sizeof(void*), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_cpose, cur_pose, 7 * sizeof(double), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        a.seeds = d_seeds; a.seeds_new = d_new; a.seeds_out = d_out; a.outcome = d_outc; a.points = d_points;
+        a.cand_points = d_cpts; a.cand_seed = d_cseed; a.counts = d_counts; a.kf_imgs = d_kimg; a.kf_poses = d_kpose;
+        a.cur_img = cur_set->d_base + (size_t)cur_frame * cur_set->stride;
+        a.cur_pose = d_cpose;
+        a.n = n; a.width = cam->width; a.height = cam->height;
+        a.fx = cam->fx; a.fy = cam->fy; a.cx = cam->cx; a.cy = cam->cy;
+        a.err_angle = std::atan(1.0 / (2.0 * cam->fx)) * 2.0;  // src/depth_estimator.cpp:202-206 (pixel noise 1)
+        svo::launch_depth_update(a, s);
+        e = hipGetLastError();
+    }
+    int32_t counts[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(counts, d_counts, sizeof(counts), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) e = hipMemcpyAsync(seeds, d_out, counts[0] * sizeof(svo_depth_seed), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && outcome) e = hipMemcpyAsync(outcome, d_outc, n * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(cand_points, d_cpts, counts[1] * 3 * sizeof(double), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(cand_seed, d_cseed, counts[1] * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    for (void* p : {(void*)d_seeds, (void*)d_new, (void*)d_out, (void*)d_outc, (void*)d_cseed, (void*)d_counts,
+                    (void*)d_points, (void*)d_cpts, (void*)d_kpose, (void*)d_cpose, (void*)d_kimg})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_depth_update: %s", hipGetErrorString(e));
+    *n_out = counts[0];
+    *n_cand = counts[1];
     return SVO_OK;
 }
 

@@ -82,4 +82,22 @@ struct FeatureAlignArgs {
 };
 void launch_feature_align(const FeatureAlignArgs& a, hipStream_t s);
 
+struct DepthArgs {
+    const svo_depth_seed* seeds;     // [n] input state
+    svo_depth_seed* seeds_new;       // [n] state after the update (scratch)
+    svo_depth_seed* seeds_out;       // [n] survivors, compacted (stable)
+    int32_t* outcome;                // [n] SVO_DEPTH_*
+    double* points;                  // [n][3] candidate point of a converged seed (scratch)
+    double* cand_points;             // [n][3] candidates in the update loop's order
+    int32_t* cand_seed;              // [n] their seed index
+    int32_t* counts;                 // [2] survivors, candidates
+    const uint8_t* const* kf_imgs;   // [n_kf] level-0 intensity image of each keyframe
+    const double* kf_poses;          // [n_kf][7]
+    const uint8_t* cur_img;          // level-0 intensity image of the current frame
+    const double* cur_pose;          // [7]
+    int32_t n, width, height;
+    double fx, fy, cx, cy, err_angle;
+};
+void launch_depth_update(const DepthArgs& a, hipStream_t s);
+
 }  // namespace svo

@@ -84,3 +84,64 @@ def make_pair(seed=SEED_BASE, n_features=2000, patch_size=5, width=1241, height=
 def gradient_fraction(img, thr=50):
     img = np.ascontiguousarray(img, np.uint8)
     return lib().svo_synth_gradient_fraction(_p(img), img.shape[1], img.shape[0], thr)
+
+
+@dataclass
+class DepthProblem:
+    """Config 5: seeds on the keyframe's features (no point yet) refined against cur."""
+    camera: dict
+    kf_img: np.ndarray
+    cur_img: np.ndarray
+    kf_pose: np.ndarray
+    cur_pose: np.ndarray
+    px: np.ndarray        # (n, 2) keyframe pixel of each seed's feature
+    bearing: np.ndarray   # (n, 3)
+    depth: np.ndarray     # (n,) true distance along the bearing (for checks only)
+    depth_mean: float     # initialisation like src/system.cpp:259 / :433: median depth, 0.5 * min depth
+    depth_min: float
+
+
+def make_depth_problem(seed=SEED_BASE, n_seeds=2000, nthreads=8):
+    """The lastKF of a synthetic pair is the keyframe, the pair's cur frame (true pose) the new frame."""
+    s = make_pair(seed=seed, n_features=2 * n_seeds, nthreads=nthreads)
+    sl = slice(s.n_ref, s.n_ref + min(s.n_kf, n_seeds))
+    kf = s.kf_pose
+    # keyframe centre C = -R^T t; distance along the bearing = |P - C|
+    q, t = kf[:4], kf[4:]
+    x, y, z, w = q
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    C = -R.T @ t
+    d = np.linalg.norm(s.point[sl] - C, axis=1)
+    return DepthProblem(s.camera, s.kf_img, s.cur_img, s.kf_pose.copy(), s.cur_true_pose.copy(), s.px[sl].copy(),
+                        s.bearing[sl].copy(), d, float(np.median(d)), float(0.5 * d.min()))
+
+
+def make_shifted_plane(seed=7, width=320, height=120, fx=300.0, depth=10.0, disparity=48, n_seeds=64,
+                       depth_min=1.5):
+    """A fronto-parallel textured plane at `depth` seen from the keyframe (identity pose) and from a
+    camera moved sideways by depth * disparity / fx: the cur image is the keyframe image shifted left by
+    `disparity` pixels, so the epipolar search must find every seed `disparity` px to the left.  The
+    small depth_min gives a wide inverse-depth range (mu +- var), so the search scans ~10 steps."""
+    rng = np.random.default_rng(seed)
+    coarse = rng.uniform(0, 255, ((height + disparity) // 4 + 3, (width + disparity) // 4 + 3))
+    yy, xx = np.mgrid[0:height + disparity, 0:width + disparity] / 4.0
+    y0, x0 = np.floor(yy).astype(int), np.floor(xx).astype(int)
+    fy_, fx_ = yy - y0, xx - x0
+    tex = ((1 - fy_) * ((1 - fx_) * coarse[y0, x0] + fx_ * coarse[y0, x0 + 1]) +
+           fy_ * ((1 - fx_) * coarse[y0 + 1, x0] + fx_ * coarse[y0 + 1, x0 + 1]))
+    tex = np.clip(tex, 0, 255).astype(np.uint8)
+    kf_img = np.ascontiguousarray(tex[:height, :width])
+    cur_img = np.ascontiguousarray(tex[:height, disparity:disparity + width])
+    cam = dict(fx=fx, fy=fx, cx=width / 2.0, cy=height / 2.0, width=width, height=height)
+    base = depth * disparity / fx
+    cur_pose = np.array([0, 0, 0, 1, -base, 0, 0], np.float64)  # camera centre at (+base, 0, 0)
+    us = rng.uniform(disparity + 30, width - 30, n_seeds)
+    vs = rng.uniform(20, height - 20, n_seeds)
+    px = np.stack([us, vs], 1)
+    b = np.stack([(us - cam["cx"]) / fx, (vs - cam["cy"]) / fx, np.ones(n_seeds)], 1)
+    bearing = b / np.linalg.norm(b, axis=1, keepdims=True)
+    d = depth / bearing[:, 2]  # distance along the bearing to the plane z = depth
+    return DepthProblem(cam, kf_img, cur_img, np.array([0, 0, 0, 1, 0, 0, 0], np.float64), cur_pose, px, bearing, d,
+                        float(np.median(d) * 1.03), float(depth_min))
