@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the single-core CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-core CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the config 3 / config 5 lines")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC traffic summary of this workload (tools/pmc_traffic.py output)")
     return ap.parse_args()
@@ -158,12 +159,68 @@ def main():
                           "frames_per_s": round(3 * P / (pyr_ms * 1e-3), 1)},
         "status_counts": {svo_amd.STATUS_NAMES[int(k)]: int(v) for k, v in zip(*np.unique(status, return_counts=True))},
     }
+    if not args.no_secondary:
+        out["secondary"] = secondary(args, ctx, scenes[0], cam, camera)
     if not args.no_cpu and world == 1:
         out.update(cpu_baseline(args, scenes, poses, L, patch, nthreads))
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def secondary(args, ctx, scene, cam, camera, reps=20):
+    """BASELINE configs 3 and 5 on this GPU, through the synchronous C-ABI calls (each call includes its
+    H2D / D2H copies and device allocations: end-to-end per call, not kernel time), with the oracle's
+    single-thread time on the same input beside it."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # noqa: E402  (CPU baseline only)
+    res = {}
+    # config 3: FeatureAlignment, 2000 candidates, level-0 gradients of the ref and cur frames
+    ps = svo_amd.PyramidSet(2, cam["width"], cam["height"], 1, ctx)
+    ps.upload(0, np.stack([scene.ref_img, scene.cur_img]))
+    ps.build()
+    rng = np.random.default_rng(3)
+    n = min(2000, len(scene.px))
+    ref_px = np.ascontiguousarray(scene.px[:n])
+    init = ref_px + rng.uniform(-1.5, 1.5, ref_px.shape)
+    rg, cg = O.build_pyramid(scene.ref_img, 1)[1], O.build_pyramid(scene.cur_img, 1)[1]
+    for p in (8, 7):
+        fa = svo_amd.FeatureAlignment(p, ctx=ctx)
+        px = np.ascontiguousarray(init.copy())
+        fa.align_batch(ps, 0, ps, 1, ref_px, px, camera)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            px = np.ascontiguousarray(init.copy())
+            fa.align_batch(ps, 0, ps, 1, ref_px, px, camera)
+        g = (time.perf_counter() - t0) / reps
+        t0 = time.perf_counter()
+        pxc, _, _ = O.feature_align(scene.camera, p, rg.reshape(cam["height"], cam["width"]),
+                                    cg.reshape(cam["height"], cam["width"]), ref_px, init)
+        c = time.perf_counter() - t0
+        res[f"config3_feature_align_p{p}"] = {
+            "candidates": n, "gpu_ms_per_call": round(g * 1e3, 4), "candidates_per_s": round(n / g, 1),
+            "cpu_ms_1_thread": round(c * 1e3, 3), "bitexact_vs_oracle": bool(np.array_equal(px, pxc))}
+    # config 5: depth-filter update, 2000 seeds on the keyframe against the cur frame
+    dp = synth.make_depth_problem(n_seeds=2000)
+    ds = svo_amd.PyramidSet(2, cam["width"], cam["height"], 1, ctx)
+    ds.upload(0, np.stack([dp.kf_img, dp.cur_img]))
+    ds.build()
+    seeds = svo_amd.depth_seeds(dp.px, dp.bearing, dp.depth_mean, dp.depth_min)
+    out = svo_amd.depth_update(camera, [(ds, 0, dp.kf_pose)], (ds, 1), dp.cur_pose, seeds, ctx)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        svo_amd.depth_update(camera, [(ds, 0, dp.kf_pose)], (ds, 1), dp.cur_pose, seeds, ctx)
+    g = (time.perf_counter() - t0) / reps
+    oseeds = O.make_seeds(dp.px, dp.bearing, dp.depth_mean, dp.depth_min)
+    t0 = time.perf_counter()
+    oc = O.depth_update(dp.camera, [dp.kf_img], dp.kf_pose[None], dp.cur_img, dp.cur_pose, oseeds)
+    c = time.perf_counter() - t0
+    res["config5_depth_filter"] = {
+        "seeds": len(seeds), "gpu_ms_per_call": round(g * 1e3, 4), "seeds_per_s": round(len(seeds) / g, 1),
+        "cpu_ms_1_thread": round(c * 1e3, 3), "outcomes": np.bincount(out[1], minlength=5).tolist(),
+        "outcomes_match_oracle": bool(np.array_equal(out[1], oc[1]))}
+    return res
 
 
 def cpu_baseline(args, scenes, gpu_poses, L, patch, nthreads):
