@@ -219,9 +219,13 @@ __global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
 // formula whenever x1 = floor(u) + kx and y1 = floor(v) + ky.  A feature where u + kx rounds up to the
 // next integer (x1 = floor(u) + kx + 1) takes the per-pixel path instead.
 template <int kHalf>
-__global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual_kernel(AlignArgs a, int level) {
+__global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual_kernel(AlignArgs a, int level) {
     using G = Win<kHalf>;
     constexpr int h = G::h, side = G::side, RB = G::RB, NW = G::RW;
+    // keys are staged in LDS as [pixel][feature] and written as whole 16-B pieces of the slot rows (one
+    // 2-B store per lane and pixel wrote each 128-B line in many partial requests: 2.8x the key bytes)
+    constexpr bool kLds = G::A * kLaneFeats * 2 <= 32768;
+    __shared__ __attribute__((aligned(16))) uint16_t kbuf[kLds ? G::A : 1][kLaneFeats];
     int pair, chunk;
     xcd_pair_chunk(a.chunks, pair, chunk);
     if (pair >= a.n_pairs) return;
@@ -229,15 +233,19 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual
     if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
     const int nf = P.n_ref + P.n_kf, fstride = slot_stride(nf);
-    const int f = chunk * kLaneFeats + (int)threadIdx.x;
-    if (f >= fstride) return;
+    const int tid = (int)threadIdx.x, f0 = chunk * kLaneFeats, f = f0 + tid;
+    if (f0 >= fstride) return;  // whole workgroup
     const int W = a.geom.w[level], H = a.geom.h[level];
     const int64_t loff = a.geom.off[level];
     const double scale = 1.0 / (double)(1 << level);
     const int border = h + 2;
-    // key of slot (k, f) at keys[k * fstride + f] (slot_store16: scalar row offset, lane offset)
+    // key of slot (k, f) at keys[k * fstride + f]
     const __amdgpu_buffer_rsrc_t keys = slot_rsrc(a.keys + (int64_t)pair * a.key_stride, a.key_stride * 2);
     const uint32_t fo = (uint32_t)f;
+    auto put = [&](int k, uint16_t key) {
+        if constexpr (kLds) kbuf[k][tid] = key;
+        else slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), key);
+    };
     int vis = 0;
     double ur = 0.0, vr = 0.0, cu = 0.0, cv = 0.0;
     if (f < nf) {
@@ -264,63 +272,74 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 2) align_residual
         a.fvis[gf] = (uint8_t)vis;
     }
     if (vis != 3) {
+        if (f < fstride) {
 #pragma unroll
-        for (int k = 0; k < G::A; ++k) slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), 0xFFFF);
-        return;
-    }
-    const uint8_t* const rplane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
-    const uint8_t* const cplane = P.cur_pyr + loff;
-    const int ru = (int)floor(ur), rv = (int)floor(vr), qu = (int)floor(cu), qv = (int)floor(cv);
-    double rwx[side], cwx[side];  // x - x1 per patch column (y - y1 per patch row: formed in the row loop)
-    bool fast = true;
-#pragma unroll
-    for (int k = 0; k < side; ++k) {
-        const double d = (double)(k - h);
-        const double xr = ur + d, xc = cu + d;
-        const int xr1 = (int)xr, xc1 = (int)xc;
-        fast = fast && xr1 == ru + k - h && xc1 == qu + k - h && (int)(vr + d) == rv + k - h && (int)(cv + d) == qv + k - h;
-        rwx[k] = xr - (double)xr1;
-        cwx[k] = xc - (double)xc1;
-    }
-    if (fast) {
-        uint32_t rrow[RB][NW], crow[RB][NW];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            load_row<G::RD>(rplane, (uint32_t)((rv - h + r) * W + (ru - h)), rrow[r]);
-            load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
-        }
-        double rprev[side], cprev[side];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            double rcur[side], ccur[side];
-#pragma unroll
-            for (int kx = 0; kx < side; ++kx) {  // (x2 - x) I(y, x1) + (x - x1) I(y, x2)
-                rcur[kx] = (1.0 - rwx[kx]) * wbyte(rrow[r], kx) + rwx[kx] * wbyte(rrow[r], kx + 1);
-                ccur[kx] = (1.0 - cwx[kx]) * wbyte(crow[r], kx) + cwx[kx] * wbyte(crow[r], kx + 1);
-            }
-            if (r > 0) {
-                const int ky = r - 1;
-                const double d = (double)(ky - h), yr = vr + d, yc = cv + d;
-                const double rwy = yr - (double)(rv + ky - h), cwy = yc - (double)(qv + ky - h);  // y - y1
-#pragma unroll
-                for (int kx = 0; kx < side; ++kx) {  // (y2 - y) a + (y - y1) b
-                    const double T = (1.0 - rwy) * rprev[kx] + rwy * rcur[kx];
-                    const double I = (1.0 - cwy) * cprev[kx] + cwy * ccur[kx];
-                    const uint32_t k = (uint32_t)((ky * side + kx) * fstride);
-                    slot_store16(keys, 2 * fo, 2 * k, res_key(I - T));
-                }
-            }
-#pragma unroll
-            for (int kx = 0; kx < side; ++kx) { rprev[kx] = rcur[kx]; cprev[kx] = ccur[kx]; }
+            for (int k = 0; k < G::A; ++k) put(k, 0xFFFF);
         }
     } else {
-        for (int ky = 0; ky < side; ++ky)
-            for (int kx = 0; kx < side; ++kx) {
-                const double T = bilinear_d(rplane, W, ur + (double)(kx - h), vr + (double)(ky - h));
-                const double I = bilinear_d(cplane, W, cu + (double)(kx - h), cv + (double)(ky - h));
-                const uint32_t k = (uint32_t)((ky * side + kx) * fstride);
-                slot_store16(keys, 2 * fo, 2 * k, res_key(I - T));
+        const uint8_t* const rplane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
+        const uint8_t* const cplane = P.cur_pyr + loff;
+        const int ru = (int)floor(ur), rv = (int)floor(vr), qu = (int)floor(cu), qv = (int)floor(cv);
+        double rwx[side], cwx[side];  // x - x1 per patch column (y - y1 per patch row: formed in the row loop)
+        bool fast = true;
+#pragma unroll
+        for (int k = 0; k < side; ++k) {
+            const double d = (double)(k - h);
+            const double xr = ur + d, xc = cu + d;
+            const int xr1 = (int)xr, xc1 = (int)xc;
+            fast = fast && xr1 == ru + k - h && xc1 == qu + k - h && (int)(vr + d) == rv + k - h &&
+                   (int)(cv + d) == qv + k - h;
+            rwx[k] = xr - (double)xr1;
+            cwx[k] = xc - (double)xc1;
+        }
+        if (fast) {
+            uint32_t rrow[RB][NW], crow[RB][NW];
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                load_row<G::RD>(rplane, (uint32_t)((rv - h + r) * W + (ru - h)), rrow[r]);
+                load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
             }
+            double rprev[side], cprev[side];
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+                double rcur[side], ccur[side];
+#pragma unroll
+                for (int kx = 0; kx < side; ++kx) {  // (x2 - x) I(y, x1) + (x - x1) I(y, x2)
+                    rcur[kx] = (1.0 - rwx[kx]) * wbyte(rrow[r], kx) + rwx[kx] * wbyte(rrow[r], kx + 1);
+                    ccur[kx] = (1.0 - cwx[kx]) * wbyte(crow[r], kx) + cwx[kx] * wbyte(crow[r], kx + 1);
+                }
+                if (r > 0) {
+                    const int ky = r - 1;
+                    const double d = (double)(ky - h), yr = vr + d, yc = cv + d;
+                    const double rwy = yr - (double)(rv + ky - h), cwy = yc - (double)(qv + ky - h);  // y - y1
+#pragma unroll
+                    for (int kx = 0; kx < side; ++kx) {  // (y2 - y) a + (y - y1) b
+                        const double T = (1.0 - rwy) * rprev[kx] + rwy * rcur[kx];
+                        const double I = (1.0 - cwy) * cprev[kx] + cwy * ccur[kx];
+                        put(ky * side + kx, res_key(I - T));
+                    }
+                }
+#pragma unroll
+                for (int kx = 0; kx < side; ++kx) { rprev[kx] = rcur[kx]; cprev[kx] = ccur[kx]; }
+            }
+        } else {
+            for (int ky = 0; ky < side; ++ky)
+                for (int kx = 0; kx < side; ++kx) {
+                    const double T = bilinear_d(rplane, W, ur + (double)(kx - h), vr + (double)(ky - h));
+                    const double I = bilinear_d(cplane, W, cu + (double)(kx - h), cv + (double)(ky - h));
+                    put(ky * side + kx, res_key(I - T));
+                }
+        }
+    }
+    if constexpr (kLds) {
+        __syncthreads();
+        const int per_row = (fstride - f0 < kLaneFeats ? fstride - f0 : kLaneFeats) / 8;  // 16-B pieces
+        uint16_t* const kp = a.keys + (int64_t)pair * a.key_stride + f0;
+        for (int idx = tid; idx < G::A * per_row; idx += kLaneFeats) {
+            const int k = idx / per_row, c8 = idx - k * per_row;
+            *reinterpret_cast<uint4*>(kp + (int64_t)k * fstride + 8 * c8) =
+                *reinterpret_cast<const uint4*>(&kbuf[k][8 * c8]);
+        }
     }
 }
 
@@ -377,7 +396,7 @@ struct SlotSrc {
 
 // Exact residual of every slot (+inf = invisible) into the pair's scratch row, for the exact paths of K2
 // (overfull bins; a neighbour the bin bracket cannot settle): four slots in flight per lane.
-__device__ void materialize(const SlotSrc& res, int Ms) {
+__device__ __forceinline__ void materialize(const SlotSrc& res, int Ms) {
     for (int s0 = threadIdx.x; s0 < Ms; s0 += 4 * kSelThreads) {
         double v[4];
 #pragma unroll
@@ -595,7 +614,7 @@ __device__ void cand_select(SelShared& sh, uint32_t n, uint32_t kk, bool want_lo
 
 // radix fallback inside one overfull bin: exact k-th among values v with sel_bin(v) == bin
 template <bool kMad>
-__device__ double radix_in_bin(SelShared& sh, const SlotSrc& res, int Ms, uint32_t bin, uint32_t k,
+__device__ __forceinline__ double radix_in_bin(SelShared& sh, const SlotSrc& res, int Ms, uint32_t bin, uint32_t k,
                                double med) {
     const int tid = threadIdx.x;
     if (tid == 0) { sh.sel_prefix = 0; sh.sel_bits = 0; sh.sel_k = k; }
@@ -629,7 +648,7 @@ __device__ double radix_in_bin(SelShared& sh, const SlotSrc& res, int Ms, uint32
 
 // (k-1)-th order statistic from the k-th (hi): hi itself if at most k-1 values are < hi, else max(<hi)
 template <bool kMad>
-__device__ double lower_neighbour_sweep(SelShared& sh, const SlotSrc& res, int Ms, uint32_t k, double hi,
+__device__ __forceinline__ double lower_neighbour_sweep(SelShared& sh, const SlotSrc& res, int Ms, uint32_t k, double hi,
                                         double med) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t less = 0;
@@ -653,7 +672,7 @@ __device__ double lower_neighbour_sweep(SelShared& sh, const SlotSrc& res, int M
 // src/algorithm.cpp:845-851; mid == 0 reads vec[mid]); Ms = slots swept.  sh.hist holds the value-bin
 // histogram.
 template <bool kMad>
-__device__ double block_median(SelShared& sh, const SlotSrc& res, int M, int Ms, uint32_t n, double med) {
+__device__ __forceinline__ double block_median(SelShared& sh, const SlotSrc& res, int M, int Ms, uint32_t n, double med) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t mid = n / 2;
     const bool want_lo = ((M & 1) == 0) && mid > 0;
