@@ -141,6 +141,26 @@ __device__ __forceinline__ double slot_load(__amdgpu_buffer_rsrc_t rs, uint32_t 
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff, 0));
 }
 
+// (x, y) -> (x with its upper kSpan-lane blocks replaced by y's lower ones, y with its lower blocks replaced
+// by x's upper ones): v_permlane32_swap / v_permlane16_swap on both 32-bit halves.  x + y then holds
+// x's pair sums in the blocks with lane bit log2(kSpan) clear and y's where it is set.
+template <int kSpan>
+__device__ __forceinline__ void lane_swap(double& x, double& y) {
+    const uint2 a = __builtin_bit_cast(uint2, x), b = __builtin_bit_cast(uint2, y);
+    uint2 na, nb;
+    if constexpr (kSpan == 32) {
+        const auto lo = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+        const auto hi = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+        na = make_uint2(lo[0], hi[0]); nb = make_uint2(lo[1], hi[1]);
+    } else {
+        const auto lo = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+        const auto hi = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+        na = make_uint2(lo[0], hi[0]); nb = make_uint2(lo[1], hi[1]);
+    }
+    x = __builtin_bit_cast(double, na);
+    y = __builtin_bit_cast(double, nb);
+}
+
 // 16-bit monotone key of a residual for K2's sweeps: floor((r + 64) * 512) clamped to [0, kKeyMax];
 // 0xFFFF marks an invisible slot.  key >> 4 is exactly the value bin floor((r + 64) * 32) of K2.
 __device__ __forceinline__ uint16_t res_key(double r) {
@@ -1012,7 +1032,7 @@ __device__ void pair_step(const AlignArgs& a, PairState& S, int level, int pair,
 // r^2 / c^2 as r^2 * (1 / c^2) (rounding only); H, g and chi2 match the reference within the tolerances of
 // tests/test_gpu_parity.py.
 template <int kHalf>
-__global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, int level) {
+__global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_kernel(AlignArgs a, int level) {
     using G = Win<kHalf>;
     constexpr int h = G::h, side = G::side, WB = G::WB, NW = G::WW;
     __shared__ SolveShared ssh;
@@ -1060,8 +1080,10 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
 #pragma unroll
         for (int r = 0; r < G::RB; ++r) load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
         double sxx = 0.0, sxy = 0.0, syy = 0.0, sxr = 0.0, syr = 0.0, chi = 0.0;
-        double P3[side], P2[side], P1[side], P0[side], D2[side], D1[side], D0[side];  // P(R-3..R), D(R-2..R)
+        // rolling row state: P(R-2), P(R-1) at the pixel columns, E(R-1) = P(R) - P(R-2), D(R-2), D(R-1)
+        double P2[side], P1[side], E1[side], D2[side], D1[side];
         double cprev[side];  // cur row blends of patch row ky (window row ky)
+        const double hgy = 0.5 * gy, hfy = 0.5 * fy;  // the 1/2 of the central differences, folded
 #pragma unroll
         for (int kx = 0; kx < side; ++kx) cprev[kx] = fma(cfx, wbyte(crow[0], kx + 1), cgx * wbyte(crow[0], kx));
 #pragma unroll
@@ -1069,27 +1091,21 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
             double hv[2 * h + 3];
 #pragma unroll
             for (int cc = 0; cc < 2 * h + 3; ++cc) hv[cc] = fma(fx, wbyte(row[R], cc + 1), gx * wbyte(row[R], cc));
-#pragma unroll
-            for (int kx = 0; kx < side; ++kx) {
-                P3[kx] = P2[kx]; P2[kx] = P1[kx]; P1[kx] = P0[kx];
-                P0[kx] = hv[kx + 1];  // window column of cell floor(u) + kx - h
-                D2[kx] = D1[kx];
-                D1[kx] = D0[kx];
-                D0[kx] = hv[kx + 2] - hv[kx];
-            }
             if (R >= 3) {  // pixel row ky: cell row R0 = ky + 1 = R - 2
                 const int ky = R - 3;
 #pragma unroll
                 for (int kx = 0; kx < side; ++kx) {
+                    const double P0 = hv[kx + 1];     // window column of cell floor(u) + kx - h
+                    const double E0 = P0 - P2[kx];    // E(R0 + 1); E1 = E(R0)
                     const double ccur = fma(cfx, wbyte(crow[ky + 1], kx + 1), cgx * wbyte(crow[ky + 1], kx));
                     const double I = fma(cfy, ccur, cgy * cprev[kx]);
                     cprev[kx] = ccur;
                     const double T = fma(fy, P1[kx], gy * P2[kx]);
                     const double r = I - T;  // the residual of K1 up to rounding (shared weights)
-                    const double dx = 0.5 * (gy * D2[kx] + fy * D1[kx]);
-                    const double dy = 0.5 * (gy * (P1[kx] - P3[kx]) + fy * (P0[kx] - P2[kx]));
+                    const double dx = fma(hfy, D1[kx], hgy * D2[kx]);
+                    const double dy = fma(hfy, E0, hgy * E1[kx]);
                     const double r2 = r * r;
-                    const double tt = 1.0 - r2 * inv_c2;
+                    const double tt = fma(-r2, inv_c2, 1.0);
                     const double w = fabs(r) <= c ? tt * tt : 0.0;  // Tukey (src/optimizer.cpp:502-511)
                     const double wdx = w * dx, wdy = w * dy;
                     sxx = fma(wdx, dx, sxx);
@@ -1100,25 +1116,52 @@ __global__ void __launch_bounds__(kLaneFeats) align_weights_kernel(AlignArgs a, 
                     chi = fma(r2, w, chi);
                 }
             }
+#pragma unroll
+            for (int kx = 0; kx < side; ++kx) {
+                const double P0 = hv[kx + 1];
+                if (R >= 2) E1[kx] = P0 - P2[kx];
+                P2[kx] = P1[kx];
+                P1[kx] = P0;
+                D2[kx] = D1[kx];
+                D1[kx] = hv[kx + 2] - hv[kx];
+            }
         }
-        // J row = dx * Jimg0 + dy * Jimg1 (image Jacobian at the WORLD point, :163, :194-248): the 21 lower
-        // H terms (row-major lower triangle), the 6 g terms and chi2 of this feature
+        // J row = dx * a + dy * b with the image Jacobian rows a, b at the WORLD point (:163, :194-248;
+        // a[1] = b[0] = 0).  Per feature sum_px w J J^T = a u^T + b v^T with u = Sxx a + Sxy b,
+        // v = Sxy a + Syy b: the 21 lower H terms (row-major lower triangle), the 6 g terms and chi2
         double ja[6], jb[6];
         image_jac(pw, a.fx / dom, a.fy / dom, ja, jb);
+        double u[6], v[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            u[i] = i == 0 ? sxx * ja[0] : (i == 1 ? sxy * jb[1] : fma(sxx, ja[i], sxy * jb[i]));
+            v[i] = i == 0 ? sxy * ja[0] : (i == 1 ? syy * jb[1] : fma(sxy, ja[i], syy * jb[i]));
+        }
         int t = 0;
 #pragma unroll
         for (int i = 0; i < 6; ++i)
 #pragma unroll
-            for (int j = 0; j <= i; ++j) {
-                acc[t++] = (ja[i] * ja[j]) * sxx + (ja[i] * jb[j] + jb[i] * ja[j]) * sxy + (jb[i] * jb[j]) * syy;
-            }
+            for (int j = 0; j <= i; ++j)
+                acc[t++] = i == 0 ? ja[0] * u[j] : (i == 1 ? jb[1] * v[j] : fma(ja[i], u[j], jb[i] * v[j]));
 #pragma unroll
-        for (int i = 0; i < 6; ++i) acc[21 + i] = ja[i] * sxr + jb[i] * syr;
+        for (int i = 0; i < 6; ++i)
+            acc[21 + i] = i == 0 ? ja[0] * sxr : (i == 1 ? jb[1] * syr : fma(ja[i], sxr, jb[i] * syr));
         acc[27] = chi;
     }
-    // halving exchange: after the steps of offsets 32..2 lane L holds term L >> 1 (half of it)
+    // halving exchange: after the steps of offsets 32..2 lane L holds term L >> 1 (half of it).  The
+    // steps across 32 and 16 lanes are CDNA4 permlane swaps (two terms per swap pair, no selects)
 #pragma unroll
-    for (int o = 32, n = 32; o >= 2; o >>= 1, n >>= 1) {
+    for (int q = 0; q < 16; ++q) {
+        lane_swap<32>(acc[q], acc[q + 16]);
+        acc[q] += acc[q + 16];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        lane_swap<16>(acc[q], acc[q + 8]);
+        acc[q] += acc[q + 8];
+    }
+#pragma unroll
+    for (int o = 8, n = 8; o >= 2; o >>= 1, n >>= 1) {
         const bool up = (lane & o) != 0;
 #pragma unroll
         for (int q = 0; q < n / 2; ++q) {
