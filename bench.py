@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--patch", type=int, default=5)
     ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic scenes per rank")
+    ap.add_argument("--feature-order", choices=("cell", "shuffled"), default="cell",
+                    help="cell: features in the order the reference detector emits them (30-px grid cells row by "
+                         "row, src/feature_selection.cpp:103-141); shuffled: random order")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the single-core CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-core CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -75,8 +78,9 @@ def main():
     D = max(1, min(args.distinct, P))
     nthreads = max(1, min(16, os.cpu_count() or 1))
     first, _ = shard.pair_block(world * P, rank, world)  # this rank's block of the job's world * P pairs
-    scenes = [synth.make_pair(seed=synth.SEED_BASE + first + i, n_features=nf, patch_size=patch, nthreads=nthreads)
-              for i in range(D)]
+    cell = 30 if args.feature_order == "cell" else 0  # config "cell_pixel_size": 30
+    scenes = [synth.make_pair(seed=synth.SEED_BASE + first + i, n_features=nf, patch_size=patch, nthreads=nthreads,
+                              cell_order=cell) for i in range(D)]
     cam = scenes[0].camera
     camera = svo_amd.PinholeCamera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"])
 
@@ -146,11 +150,12 @@ def main():
         "config": {"workload": f"config 2: ImageAlignment::align, {nf} feats ({nf // 2} ref + {nf - nf // 2} lastKF), "
                                f"patch {patch}, {L}-level pyramid, {cam['width']}x{cam['height']}, {P} pairs/GPU",
                    "pairs_per_gpu": P, "features": nf, "levels": L, "patch": patch, "distinct_scenes": D,
+                   "feature_order": args.feature_order,
                    "parallelism": f"pairs sharded over {world} GPU(s), no collective"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "kernel": f"align chain: K0 + {L} levels x (K1 residual, K2 robust scale, K3 weights + LM step), "
-                               f"{1 + 3 * L} launches per chain, 2 concurrent half-batch chains",
+                     "kernel": f"align chain: {L} levels x (K1 residual [+ pair init at the first level], K2 robust scale, "
+                               f"K3 weights + LM step), {3 * L} launches per chain, 2 concurrent half-batch chains",
                      "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": b_pair * P,
                      "algorithmic_bytes_per_pair": b_pair, "traffic_source": traffic_src,
                      "stages_ms": {k: round(v, 4) for k, v in stages.items()},

@@ -2,9 +2,10 @@
 //
 // A batch holds n_pairs independent frame pairs.  The coarse-to-fine chain runs as
 // stage kernels over all pairs of the batch, enqueued back to back on the context stream:
-//   K0 init      thread / feature : X_w = T_f^-1 (bearing * |P - C_f|) (:153-155); per-pair state
 //   per level (max..min):
-//   K1 residual  lane / feature (64-lane workgroups): ref visibility (border rule :140-149), projection
+//   K1 residual  lane / feature (256-lane workgroups); at the first level it also forms the world points
+//                X_w = T_f^-1 (bearing * |P - C_f|) (:153-155) and the pair state (init_pair)
+//                ref visibility (border rule :140-149), projection
 //                pose * X_w into cur (:320-340); the feature's ref and cur windows are loaded into
 //                registers, one 16-B load per window row, and r = I_cur - T_ref (:359) is formed with the
 //                reference's own bilinear arithmetic in separable form: each window row's horizontal
@@ -195,38 +196,40 @@ int align_chunks(int max_f, int half, int feat_iters) {
     return (max_f + kLaneFeats - 1) / kLaneFeats;
 }
 
-// ------------------------------------------------------------------ K0: world points, pair state
-__global__ void __launch_bounds__(256) align_init_kernel(AlignArgs a) {
-    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid < a.n_pairs) {
-        const PairDesc& P = a.pairs[gid];
-        PairState& S = a.state[gid];
-        for (int i = 0; i < 7; ++i) S.pose[i] = P.cur_pose[i];
-        const int nf = P.n_ref + P.n_kf;
-        S.active = (P.n_ref > 0 && (int64_t)nf * a.area >= 6) ? 1 : 0;
-        S.err = P.n_ref == 0 ? 0.0 : -1.0;  // align() returns 0 (:27-28); optimizeLM returns -1 when M < 6
-        S.status = P.n_ref == 0 ? kFailed : kNonSuffPoints;
-        a.arrive[gid] = 0u;
-        svo_level_trace* tr = a.traces + gid * (a.max_level + 1);
-        for (int l = 0; l <= a.max_level; ++l) {
-            svo_level_trace t = {};
-            t.level = l;
-            t.status = kFailed;
-            tr[l] = t;
-        }
+// ------------------------------------------------------------------ pair state, world points
+// Done by the first (coarsest) level's K1 rather than a launch of its own: one pass over the batch's
+// feature records instead of two, and one launch less per chain.
+__device__ __forceinline__ bool pair_active(const PairDesc& P, int area) {
+    return P.n_ref > 0 && (int64_t)(P.n_ref + P.n_kf) * area >= 6;
+}
+
+// the pair's optimizer state before the first level (src/image_alignment.cpp:25-60): pose, status, the
+// per-level traces; one lane
+__device__ void init_pair(const AlignArgs& a, const PairDesc& P, int pair) {
+    PairState& S = a.state[pair];
+    for (int i = 0; i < 7; ++i) S.pose[i] = P.cur_pose[i];
+    S.active = pair_active(P, a.area) ? 1 : 0;
+    S.err = P.n_ref == 0 ? 0.0 : -1.0;  // align() returns 0 (:27-28); optimizeLM returns -1 when M < 6
+    S.status = P.n_ref == 0 ? kFailed : kNonSuffPoints;
+    a.arrive[pair] = 0u;
+    svo_level_trace* tr = a.traces + pair * (a.max_level + 1);
+    for (int l = 0; l <= a.max_level; ++l) {
+        svo_level_trace t = {};
+        t.level = l;
+        t.status = kFailed;
+        tr[l] = t;
     }
-    if (gid >= (int64_t)a.n_pairs * a.max_f) return;
-    const int pair = (int)(gid / a.max_f), f = (int)(gid - (int64_t)pair * a.max_f);
-    const PairDesc& P = a.pairs[pair];
-    if (f >= P.n_ref + P.n_kf || !a.has_point[gid]) return;
-    const bool is_ref = f < P.n_ref;
+}
+
+// world point of feature f (src/image_alignment.cpp:153-155): the frame's inverse pose applied to the
+// bearing scaled by the distance of the feature's point from the camera centre
+__device__ __forceinline__ V3 world_point(const AlignArgs& a, const PairDesc& P, int64_t gf, bool is_ref) {
     const SE3 T = se3_load(is_ref ? P.ref_pose : P.kf_pose);
     const V3 C = camera_in_world(T);
-    const V3 Pw{a.point[3 * gid], a.point[3 * gid + 1], a.point[3 * gid + 2]};
+    const V3 Pw{a.point[3 * gf], a.point[3 * gf + 1], a.point[3 * gf + 2]};
     const double depth = v3norm(v3sub(Pw, C));
-    const V3 pc = v3scl(V3{a.bearing[3 * gid], a.bearing[3 * gid + 1], a.bearing[3 * gid + 2]}, depth);
-    const V3 pw = se3_act(se3_inverse(T), pc);
-    a.xw[3 * gid] = pw.x; a.xw[3 * gid + 1] = pw.y; a.xw[3 * gid + 2] = pw.z;
+    const V3 pc = v3scl(V3{a.bearing[3 * gf], a.bearing[3 * gf + 1], a.bearing[3 * gf + 2]}, depth);
+    return se3_act(se3_inverse(T), pc);
 }
 
 // ------------------------------------------------------------------ K1: visibility, projection, residuals
@@ -249,9 +252,13 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
     int pair, chunk;
     xcd_pair_chunk(a.chunks, pair, chunk);
     if (pair >= a.n_pairs) return;
-    const PairState& S = a.state[pair];
-    if (!S.active) return;
     const PairDesc& P = a.pairs[pair];
+    // the first level initialises the pair (one lane) and forms the world points; its other lanes take
+    // the initial pose and the active flag from the pair record, not from the state being written
+    const bool first = level == a.max_level;
+    if (first && chunk == 0 && threadIdx.x == 0) init_pair(a, P, pair);
+    if (!(first ? pair_active(P, a.area) : a.state[pair].active != 0)) return;
+    const double* const pose = first ? P.cur_pose : a.state[pair].pose;
     const int nf = P.n_ref + P.n_kf, fstride = slot_stride(nf);
     const int tid = (int)threadIdx.x, f0 = chunk * kLaneFeats, f = f0 + tid;
     if (f0 >= fstride) return;  // whole workgroup
@@ -272,14 +279,20 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
         const int64_t gf = (int64_t)pair * a.max_f + f;
         const uint8_t hp = a.has_point[gf];  // all of the feature's loads at once (one memory round trip)
         const double pu = a.px[2 * gf], pv = a.px[2 * gf + 1];
-        const V3 pw{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
+        V3 pw{0.0, 0.0, 0.0};
+        if (!first) {
+            pw = V3{a.xw[3 * gf], a.xw[3 * gf + 1], a.xw[3 * gf + 2]};
+        } else if (hp) {
+            pw = world_point(a, P, gf, f < P.n_ref);
+            a.xw[3 * gf] = pw.x; a.xw[3 * gf + 1] = pw.y; a.xw[3 * gf + 2] = pw.z;
+        }
         if (hp) {
             ur = pu * scale;
             vr = pv * scale;
             const int ui = (int)floor(ur), vi = (int)floor(vr);
             if (!((ui - border) < 0 || (vi - border) < 0 || (ui + border) >= W || (vi + border) >= H)) {
                 vis = 1;
-                const V3 cp = se3_act(se3_load(S.pose), pw);
+                const V3 cp = se3_act(se3_load(pose), pw);
                 cu = (a.fx * (cp.x / cp.z) + a.cx) * scale;
                 cv = (a.fy * (cp.y / cp.z) + a.cy) * scale;
                 const int cui = (int)floor(cu), cvi = (int)floor(cv);
@@ -1043,7 +1056,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_
     if (pair >= a.n_pairs) return;
     PairState& S = a.state[pair];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (!S.active) {  // nothing to align: the outputs are the initial state (K0)
+    if (!S.active) {  // nothing to align: the outputs are the initial state (init_pair)
         if (level == a.min_level && chunk == 0 && tid == 0) {
             for (int i = 0; i < 7; ++i) a.pose_out[7 * pair + i] = S.pose[i];
             a.err_out[pair] = S.err;
@@ -1200,17 +1213,14 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_
 
 // ------------------------------------------------------------------ launch
 // marks (optional): an event recorded before every launch and after the last one, in launch order
-// K0, then per level K1 K2 K3 (1 + 3 * levels + 1 events)
+// start, then per level K1 K2 K3 (1 + 3 * levels + 1 events)
 template <int kHalf>
 static void launch_all(const AlignArgs& a, hipStream_t s, hipEvent_t* marks) {
     int m = 0;
     auto mark = [&]() {
         if (marks) (void)hipEventRecord(marks[m++], s);
     };
-    const int64_t nthreads = (int64_t)a.n_pairs * a.max_f;
-    const int64_t blocks = (nthreads > a.n_pairs ? nthreads : a.n_pairs) / 256 + 1;
-    mark();
-    hipLaunchKernelGGL(align_init_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    mark();  // (the pair init runs inside the first K1: the "init" interval is empty)
     const unsigned fgrid = (unsigned)((int64_t)((a.n_pairs + 7) / 8) * 8 * a.chunks);
     for (int level = a.max_level; level >= a.min_level; --level) {
         mark();

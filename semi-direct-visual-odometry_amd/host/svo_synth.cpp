@@ -192,7 +192,8 @@ static inline int grad_at(const uint8_t* im, int w, int x, int y) {
 }
 
 static int pick_features(const Scene& sc, const Cam& cam, const Pose& pose, const uint8_t* img, int count, int margin,
-                         double null_frac, Rng& rng, double* px, double* bearing, double* point, uint8_t* has_point) {
+                         double null_frac, int cell, Rng& rng, double* px, double* bearing, double* point,
+                         uint8_t* has_point) {
     std::vector<int> cand;
     for (int y = margin; y < cam.h - margin - 1; ++y)
         for (int x = margin; x < cam.w - margin - 1; ++x)
@@ -205,6 +206,11 @@ static int pick_features(const Scene& sc, const Cam& cam, const Pose& pose, cons
     for (int i = 0; i < count && i < (int)cand.size(); ++i) {  // partial Fisher-Yates
         size_t j = i + (size_t)(rng.next() % (uint64_t)(cand.size() - i));
         std::swap(cand[i], cand[j]);
+    }
+    if (cell > 0) {  // the detector's emission order: grid cells row-major, then pixel index
+        const int n = std::min(count, (int)cand.size()), cols = cam.w / cell + 1;
+        auto key = [&](int p) { return (int64_t)((p / cam.w) / cell * cols + (p % cam.w) / cell) * cam.w * cam.h + p; };
+        std::sort(cand.begin(), cand.begin() + n, [&](int a, int b) { return key(a) < key(b); });
     }
     double Rwc[3][3], C[3];
     for (int i = 0; i < 3; ++i)
@@ -242,6 +248,9 @@ typedef struct {
     double init_trans_err;     // metres (default 0.02)
     double init_rot_err_deg;   // degrees (default 0.2)
     int32_t nthreads;
+    int32_t cell_order;        // 0: features in shuffled order; c > 0: in the order FeatureSelection's
+                               // bucketing emits them (src/feature_selection.cpp:103-141): c-px grid cells
+                               // row by row (config "cell_pixel_size": 30), pixel order within a cell
 } svo_synth_config;
 
 void svo_synth_default_config(svo_synth_config* c) {
@@ -253,6 +262,7 @@ void svo_synth_default_config(svo_synth_config* c) {
     c->init_trans_err = 0.02;
     c->init_rot_err_deg = 0.2;
     c->nthreads = 1;
+    c->cell_order = 0;
 }
 
 // Renders one (last keyframe, ref, cur) triple and its features.  Returns the number of features
@@ -306,8 +316,8 @@ int32_t svo_synth_pair(const svo_synth_config* c, uint64_t seed, uint8_t* kf_img
 
     const int margin = c->patch_size / 2 + 3;
     const int want_ref = c->n_features / 2, want_kf = c->n_features - c->n_features / 2;
-    int nr = pick_features(sc, cam, P_ref, ref_img, want_ref, margin, c->null_point_fraction, rng, px, bearing, point, has_point);
-    int nk = pick_features(sc, cam, P_kf, kf_img, want_kf, margin, c->null_point_fraction, rng, px + 2 * nr, bearing + 3 * nr,
+    int nr = pick_features(sc, cam, P_ref, ref_img, want_ref, margin, c->null_point_fraction, c->cell_order, rng, px, bearing, point, has_point);
+    int nk = pick_features(sc, cam, P_kf, kf_img, want_kf, margin, c->null_point_fraction, c->cell_order, rng, px + 2 * nr, bearing + 3 * nr,
                            point + 3 * nr, has_point + nr);
     *n_ref = nr;
     *n_kf = nk;

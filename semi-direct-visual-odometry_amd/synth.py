@@ -19,7 +19,8 @@ class SynthConfig(ctypes.Structure):
                 ("fy", ctypes.c_double), ("cx", ctypes.c_double), ("cy", ctypes.c_double),
                 ("n_features", ctypes.c_int32), ("patch_size", ctypes.c_int32),
                 ("null_point_fraction", ctypes.c_double), ("init_trans_err", ctypes.c_double),
-                ("init_rot_err_deg", ctypes.c_double), ("nthreads", ctypes.c_int32)]
+                ("init_rot_err_deg", ctypes.c_double), ("nthreads", ctypes.c_int32),
+                ("cell_order", ctypes.c_int32)]
 
 
 def lib():
@@ -65,10 +66,11 @@ def default_config(**kw):
 
 
 def make_pair(seed=SEED_BASE, n_features=2000, patch_size=5, width=1241, height=376, null_point_fraction=0.0,
-              init_trans_err=0.02, init_rot_err_deg=0.2, nthreads=8):
+              init_trans_err=0.02, init_rot_err_deg=0.2, nthreads=8, cell_order=0):
+    """cell_order: 0 shuffled features; c > 0 the reference detector's order (c-px cells row by row)."""
     c = default_config(n_features=n_features, patch_size=patch_size, width=width, height=height,
                        null_point_fraction=null_point_fraction, init_trans_err=init_trans_err,
-                       init_rot_err_deg=init_rot_err_deg, nthreads=nthreads)
+                       init_rot_err_deg=init_rot_err_deg, nthreads=nthreads, cell_order=cell_order)
     H, W, N = c.height, c.width, c.n_features
     imgs = [np.zeros((H, W), np.uint8) for _ in range(3)]
     poses = [np.zeros(7) for _ in range(4)]
