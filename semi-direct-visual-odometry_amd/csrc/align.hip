@@ -142,6 +142,40 @@ __device__ __forceinline__ double slot_load(__amdgpu_buffer_rsrc_t rs, uint32_t 
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, (int)voff, (int)soff, 0));
 }
 
+// Feature windows of a window level (AlignArgs::win): per pair, the ref section (WB rows of WW dwords) then
+// the cur section (RB rows of RW dwords), each row a [feature][N dwords] plane of fstride features, so a
+// wave's access to one row is one contiguous run.  voff = the lane's feature * 4N, soff = the row's base.
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int N>
+__device__ __forceinline__ void win_store(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, const uint32_t (&v)[N]) {
+    int i = 0;
+#pragma unroll
+    for (; i + 4 <= N; i += 4)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{v[i], v[i + 1], v[i + 2], v[i + 3]}, rs, (int)(voff + 4 * i), (int)soff, 0);
+    if constexpr (N % 4 == 3) __builtin_amdgcn_raw_buffer_store_b96(u32x3{v[i], v[i + 1], v[i + 2]}, rs, (int)(voff + 4 * i), (int)soff, 0);
+    if constexpr (N % 4 == 2) __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[i], v[i + 1]}, rs, (int)(voff + 4 * i), (int)soff, 0);
+    if constexpr (N % 4 == 1) __builtin_amdgcn_raw_buffer_store_b32(v[i], rs, (int)(voff + 4 * i), (int)soff, 0);
+}
+template <int N>
+__device__ __forceinline__ void win_load(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t (&v)[N]) {
+    int i = 0;
+#pragma unroll
+    for (; i + 4 <= N; i += 4) {
+        const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(voff + 4 * i), (int)soff, 0);
+        v[i] = t.x; v[i + 1] = t.y; v[i + 2] = t.z; v[i + 3] = t.w;
+    }
+    if constexpr (N % 4 == 3) {
+        const u32x3 t = __builtin_amdgcn_raw_buffer_load_b96(rs, (int)(voff + 4 * i), (int)soff, 0);
+        v[i] = t.x; v[i + 1] = t.y; v[i + 2] = t.z;
+    }
+    if constexpr (N % 4 == 2) {
+        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(voff + 4 * i), (int)soff, 0);
+        v[i] = t.x; v[i + 1] = t.y;
+    }
+    if constexpr (N % 4 == 1) v[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(voff + 4 * i), (int)soff, 0);
+}
+
 // (x, y) -> (x with its upper kSpan-lane blocks replaced by y's lower ones, y with its lower blocks replaced
 // by x's upper ones): v_permlane32_swap / v_permlane16_swap on both 32-bit halves.  x + y then holds
 // x's pair sums in the blocks with lane bit log2(kSpan) clear and y's where it is set.
@@ -189,6 +223,10 @@ __device__ __forceinline__ int slot_stride(int nf) { return (nf + 63) & ~63; }
 }  // namespace
 
 int align_feat_iters() { return 1; }
+int align_win_dwords(int half) {
+    const int RB = 2 * half + 2, WB = 2 * half + 4;
+    return WB * ((WB + 3) / 4) + RB * ((RB + 3) / 4);
+}
 
 int align_chunks(int max_f, int half, int feat_iters) {
     (void)half;
@@ -241,7 +279,7 @@ __device__ __forceinline__ V3 world_point(const AlignArgs& a, const PairDesc& P,
 // are formed once and shared by the two patch rows that read them: bit-identical to the per-sample
 // formula whenever x1 = floor(u) + kx and y1 = floor(v) + ky.  A feature where u + kx rounds up to the
 // next integer (x1 = floor(u) + kx + 1) takes the per-pixel path instead.
-template <int kHalf>
+template <int kHalf, bool kWin>  // kWin: a window level (AlignArgs::win_levels)
 __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual_kernel(AlignArgs a, int level) {
     using G = Win<kHalf>;
     constexpr int h = G::h, side = G::side, RB = G::RB, NW = G::RW;
@@ -325,13 +363,34 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
             rwx[k] = xr - (double)xr1;
             cwx[k] = xc - (double)xc1;
         }
-        if (fast) {
-            uint32_t rrow[RB][NW], crow[RB][NW];
+        uint32_t rrow[RB][NW], crow[RB][NW];
+        if constexpr (kWin) {  // window level: K3's ref window (rows / bytes -h-1 .. h+2) and the cur window, handed on
+            uint32_t wrow[G::WB][G::WW];
 #pragma unroll
-            for (int r = 0; r < RB; ++r) {
-                load_row<G::RD>(rplane, (uint32_t)((rv - h + r) * W + (ru - h)), rrow[r]);
-                load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
+            for (int R = 0; R < G::WB; ++R) load_row<G::WD>(rplane, (uint32_t)((rv - h - 1 + R) * W + (ru - h - 1)), wrow[R]);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
+            const __amdgpu_buffer_rsrc_t ws = slot_rsrc(a.win + (int64_t)pair * a.win_stride, a.win_stride * 4);
+#pragma unroll
+            for (int R = 0; R < G::WB; ++R) win_store<G::WW>(ws, fo * (4 * G::WW), (uint32_t)(R * fstride * 4 * G::WW), wrow[R]);
+            const uint32_t cbase = (uint32_t)(G::WB * G::WW * fstride * 4);
+#pragma unroll
+            for (int r = 0; r < RB; ++r) win_store<NW>(ws, fo * (4 * NW), cbase + (uint32_t)(r * fstride * 4 * NW), crow[r]);
+#pragma unroll
+            for (int r = 0; r < RB; ++r)  // K1's rows: window rows 1.., shifted by one byte
+#pragma unroll
+                for (int i = 0; i < NW; ++i)
+                    rrow[r][i] = __builtin_amdgcn_alignbyte(i + 1 < G::WW ? wrow[r + 1][i + 1] : 0u, wrow[r + 1][i], 1);
+        } else {
+            if (fast) {
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {
+                    load_row<G::RD>(rplane, (uint32_t)((rv - h + r) * W + (ru - h)), rrow[r]);
+                    load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
+                }
             }
+        }
+        if (fast) {
             double rprev[side], cprev[side];
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
@@ -1124,7 +1183,7 @@ __device__ void pair_step(const AlignArgs& a, PairState& S, int level, int pair,
 // is emitted once row R0 + 2 has been blended.  The Tukey weight uses
 // r^2 / c^2 as r^2 * (1 / c^2) (rounding only); H, g and chi2 match the reference within the tolerances of
 // tests/test_gpu_parity.py.
-template <int kHalf>
+template <int kHalf, bool kWin>  // kWin: a window level (AlignArgs::win_levels)
 __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_kernel(AlignArgs a, int level) {
     using G = Win<kHalf>;
     constexpr int h = G::h, side = G::side, WB = G::WB, NW = G::WW;
@@ -1168,10 +1227,21 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_
         const uint8_t* const plane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
         const uint8_t* const cplane = P.cur_pyr + loff;
         uint32_t row[WB][NW], crow[G::RB][G::RW];
+        if constexpr (kWin) {  // the windows K1 wrote (one contiguous run per row and wave)
+            const int fstride = slot_stride(nf);
+            const __amdgpu_buffer_rsrc_t ws = slot_rsrc(a.win + (int64_t)pair * a.win_stride, a.win_stride * 4);
+            const uint32_t fo = (uint32_t)f, cbase = (uint32_t)(WB * NW * fstride * 4);
 #pragma unroll
-        for (int R = 0; R < WB; ++R) load_row<G::WD>(plane, (uint32_t)((rv - h - 1 + R) * W + (ru - h - 1)), row[R]);
+            for (int R = 0; R < WB; ++R) win_load<NW>(ws, fo * (4 * NW), (uint32_t)(R * fstride * 4 * NW), row[R]);
 #pragma unroll
-        for (int r = 0; r < G::RB; ++r) load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
+            for (int r = 0; r < G::RB; ++r)
+                win_load<G::RW>(ws, fo * (4 * G::RW), cbase + (uint32_t)(r * fstride * 4 * G::RW), crow[r]);
+        } else {
+#pragma unroll
+            for (int R = 0; R < WB; ++R) load_row<G::WD>(plane, (uint32_t)((rv - h - 1 + R) * W + (ru - h - 1)), row[R]);
+#pragma unroll
+            for (int r = 0; r < G::RB; ++r) load_row<G::RD>(cplane, (uint32_t)((qv - h + r) * W + (qu - h)), crow[r]);
+        }
         double sxx = 0.0, sxy = 0.0, syy = 0.0, sxr = 0.0, syr = 0.0, chi = 0.0;
         // rolling row state: P(R-2), P(R-1) at the pixel columns, E(R-1) = P(R) - P(R-2), D(R-2), D(R-1)
         double P2[side], P1[side], E1[side], D2[side], D1[side];
@@ -1304,11 +1374,14 @@ static void launch_all(const AlignArgs& a, hipStream_t s, hipEvent_t* marks) {
     const unsigned fgrid = (unsigned)((int64_t)((a.n_pairs + 7) / 8) * 8 * a.chunks);
     for (int level = a.max_level; level >= a.min_level; --level) {
         mark();
-        hipLaunchKernelGGL(align_residual_kernel<kHalf>, dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+        const bool win = (a.win_levels >> level) & 1u;
+        if (win) hipLaunchKernelGGL((align_residual_kernel<kHalf, true>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+        else hipLaunchKernelGGL((align_residual_kernel<kHalf, false>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
         mark();
         hipLaunchKernelGGL(align_scale_kernel, dim3(a.n_pairs), dim3(kSelThreads), 0, s, a, level);
         mark();
-        hipLaunchKernelGGL(align_weights_kernel<kHalf>, dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+        if (win) hipLaunchKernelGGL((align_weights_kernel<kHalf, true>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+        else hipLaunchKernelGGL((align_weights_kernel<kHalf, false>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
     }
     mark();
 }

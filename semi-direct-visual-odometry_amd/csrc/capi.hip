@@ -76,6 +76,9 @@ struct svo_align_batch {
     int32_t n_pairs, max_f, half, area;
     int64_t key_stride;
     uint16_t* d_keys;
+    uint32_t* d_win;
+    int64_t win_stride;
+    uint32_t win_levels;
     svo::LevelGeom geom;
     std::vector<svo::PairDesc> h_pairs;
     std::vector<uint8_t> pair_set;
@@ -254,7 +257,8 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_keys,
-                    b->d_state, b->d_partials, b->d_arrive, b->d_fvis, b->d_cproj, b->d_scratch, b->d_pose_out, b->d_err, b->d_status, b->d_traces};
+                    b->d_state, b->d_partials, b->d_arrive, b->d_fvis, b->d_cproj, b->d_scratch, b->d_pose_out, b->d_err, b->d_status, b->d_traces,
+                    b->d_win};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -301,6 +305,18 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     ALLOC(b->d_cproj, F * 2 * sizeof(double));
     ALLOC(b->d_scratch, (size_t)n_pairs * b->key_stride * sizeof(double));
     ALLOC(b->d_keys, (size_t)n_pairs * b->key_stride * sizeof(uint16_t));
+    // window levels: where K3 re-gathering the level's planes would cost more than K1 handing over the
+    // windows (3 planes' bytes >= 4x the windows written + read); SVO_WIN_LEVELS (a level bitmask)
+    // overrides, for measurements
+    {
+        const int64_t wdw = svo::align_win_dwords(half), fpad = (max_features + 63) / 64 * 64;
+        b->win_stride = wdw * fpad;
+        b->win_levels = 0;
+        for (int l = prm->min_level; l <= prm->max_level; ++l)
+            if (3ll * b->geom.w[l] * b->geom.h[l] >= 4ll * 4 * wdw * max_features) b->win_levels |= 1u << l;
+        if (const char* ov = getenv("SVO_WIN_LEVELS")) b->win_levels = (uint32_t)strtoul(ov, nullptr, 0);
+        if (b->win_levels) ALLOC(b->d_win, (size_t)n_pairs * b->win_stride * sizeof(uint32_t));
+    }
     ALLOC(b->d_pose_out, (size_t)n_pairs * 7 * sizeof(double));
     ALLOC(b->d_err, (size_t)n_pairs * sizeof(double));
     ALLOC(b->d_status, (size_t)n_pairs * sizeof(int32_t));
@@ -392,6 +408,7 @@ static svo::AlignArgs sub_batch(const svo::AlignArgs& a, const svo_align_batch* 
     s.cproj += 2 * F;
     s.partials += (int64_t)p0 * b->chunks * 28; s.arrive += p0;
     s.keys += (int64_t)p0 * b->key_stride; s.scratch += (int64_t)p0 * b->key_stride;
+    if (s.win) s.win += (int64_t)p0 * b->win_stride;
     s.pose_out += 7 * (int64_t)p0; s.err_out += p0; s.status_out += p0;
     s.traces += (int64_t)p0 * (b->params.max_level + 1);
     s.n_pairs = n;
@@ -409,6 +426,7 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
     a.xw = b->d_xw; a.keys = b->d_keys; a.key_stride = b->key_stride; a.state = b->d_state; a.partials = b->d_partials;
     a.arrive = b->d_arrive;
+    a.win = b->d_win; a.win_stride = b->win_stride; a.win_levels = b->win_levels;
     a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.cproj = b->d_cproj; a.scratch = b->d_scratch;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
     a.n_pairs = b->n_pairs; a.pair_base = 0; a.max_f = b->max_f; a.half = b->half; a.area = b->area;

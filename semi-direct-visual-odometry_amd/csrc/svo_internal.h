@@ -53,6 +53,10 @@ struct AlignArgs {
     double* scratch;          // scratch [n_pairs][key_stride] exact residuals, written only by K2's exact paths
     uint16_t* keys;           // scratch [n_pairs][key_stride] 16-bit monotone key per slot (0xFFFF = invisible)
     int64_t key_stride;       // >= area * round_up(max_f, 64), multiple of 64
+    uint32_t* win;            // scratch [n_pairs][win_stride] feature windows of the window levels (K1 -> K3)
+    int64_t win_stride;       // dwords per pair: align_win_dwords(half) * round_up(max_f, 64)
+    uint32_t win_levels;      // bit l: at level l K1 hands each visible feature's ref / cur windows to K3
+                              // (K3 then reads them instead of gathering from the pyramid planes)
     double* pose_out;         // [n_pairs][7]
     double* err_out;          // [n_pairs]
     int32_t* status_out;      // [n_pairs]
@@ -68,6 +72,7 @@ struct AlignArgs {
 void launch_align(const AlignArgs& a, hipStream_t s, hipEvent_t* marks = nullptr);  // marks: see align.hip
 int align_max_half();  // largest patch half size the alignment kernels are instantiated for
 int align_feat_iters();                                 // feature groups per K1/K3 wave
+int align_win_dwords(int half);                         // window dwords per feature (win_stride / slots)
 int align_chunks(int max_f, int half, int feat_iters);  // K1/K3 workgroups per pair
 void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t count, hipStream_t s);
 
