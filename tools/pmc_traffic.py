@@ -3,8 +3,8 @@
 Correction per MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the bytes of a wide read,
 so it is doubled; WRITE_SIZE is taken as is.  Both are KiB per dispatch.  Traffic of one chain launch
 (= one bench step over all pairs) = sum over the chain's kernels of the per-dispatch bytes, divided by
-the number of bench steps in the profiled process (dispatches of align_init_kernel / --chains: a batch of
->= 64 pairs runs as two concurrent half-batch chains, each with its own K0).
+the number of bench steps in the profiled process: dispatches of align_scale_kernel (K2, once per level
+and chain) / (levels x --chains); a batch of >= 64 pairs runs as two concurrent half-batch chains.
 
 usage: python3 tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> --pairs P --features N --levels L
        --patch S > profiles/pmc_traffic.json
@@ -26,7 +26,7 @@ def per_kernel(pass_dir, counter):
             if "svo::align" not in name or r["Counter_Name"] != counter:
                 continue
             tot[name.split("(")[0]] += float(r["Counter_Value"]) * 1024.0
-            if "align_init_kernel" in name:
+            if "align_scale_kernel" in name:
                 runs += 1
     return tot, runs
 
@@ -39,12 +39,12 @@ def main():
     ap.add_argument("--features", type=int, default=2000)
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--patch", type=int, default=5)
-    ap.add_argument("--chains", type=int, default=2, help="K0 dispatches per bench step")
+    ap.add_argument("--chains", type=int, default=2, help="concurrent chains per bench step")
     a = ap.parse_args()
     fetch, runs_f = per_kernel(a.fetch_dir, "FETCH_SIZE")
     write, runs_w = per_kernel(a.write_dir, "WRITE_SIZE")
     assert runs_f and runs_w, "no align dispatches found"
-    runs_f, runs_w = runs_f / a.chains, runs_w / a.chains
+    runs_f, runs_w = runs_f / (a.chains * a.levels), runs_w / (a.chains * a.levels)
     kernels = sorted(set(fetch) | set(write))
     per = {k: {"read": 2.0 * fetch[k] / runs_f, "write": write[k] / runs_w} for k in kernels}
     total = sum(v["read"] + v["write"] for v in per.values())
