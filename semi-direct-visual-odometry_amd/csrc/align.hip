@@ -896,6 +896,7 @@ __global__ void __launch_bounds__(kSelThreads, 4) align_scale_kernel(AlignArgs a
     res.scale = 1.0 / (double)(1 << level);
     const uint8_t* __restrict__ fvis = a.fvis + (int64_t)pair * a.max_f;
     K2_STAMP(0, clock64());
+    K2_STAMP(14, __builtin_amdgcn_s_memrealtime());  // 100 MHz, chip-wide: workgroup start / end spread
     uint32_t nrv = 0, ncv = 0;
     for (int f = tid; f < nf; f += kSelThreads) {
         const uint8_t v = fvis[f];
@@ -1104,6 +1105,7 @@ __global__ void __launch_bounds__(kSelThreads, 4) align_scale_kernel(AlignArgs a
         S.n = n;
         S.n_ref_vis = nrv;
     }
+    K2_STAMP(15, __builtin_amdgcn_s_memrealtime());
 }
 // ------------------------------------------------------------------ K3: weights, normal equations, LM step
 namespace {

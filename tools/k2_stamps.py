@@ -57,6 +57,12 @@ def main():
         print(f"level {level}: total={tot:.0f} cyc (max {np.max(s[:, 9] - s[:, 0]):.0f})  {row}  | median cnt "
               f"med={np.median(s[:, 10] % 1000000):.0f} max={np.max(s[:, 10] % 1000000):.0f} slow={med_slow}  "
               f"mad cand med={np.median(s[:, 11]):.0f} max={np.max(s[:, 11]):.0f} slow={mad_slow}")
+        if np.any(s[:, 14]):  # realtime (100 MHz) workgroup start / end, per half-batch chain
+            for c0 in range(0, P, P // 2):
+                t0, t1 = s[c0:c0 + P // 2, 14], s[c0:c0 + P // 2, 15]
+                print(f"          chain @{c0}: starts spread {(t0.max() - t0.min()) / 100:.1f} us, "
+                      f"wg duration med {np.median(t1 - t0) / 100:.1f} us max {(t1 - t0).max() / 100:.1f} us, "
+                      f"first start -> last end {(t1.max() - t0.min()) / 100:.1f} us")
         if np.any(s[:, 13]):  # SVO_K2_DUP build: a second key sweep before the gather
             print(f"          second key sweep={np.median(s[:, 13] - s[:, 4]):.0f}  gather after it="
                   f"{np.median(s[:, 5] - s[:, 13]):.0f}")
