@@ -942,7 +942,10 @@ __global__ void __launch_bounds__(kSelThreads, 4) align_scale_kernel(AlignArgs a
         double mlo, mhi;
         if (med_fast) {
             const double eps = 1e-9;
-            mlo = bin == 0 ? -__builtin_inf() : (double)bin / kBinScale - kBinOffset - eps;
+            // need_prev: med = (largest value of bin pbin + smallest of bin) / 2 may lie below the bin,
+            // down to the midpoint of the two bins' lower edges
+            const uint32_t lob = need_prev ? pbin : bin;
+            mlo = lob == 0 ? -__builtin_inf() : ((double)lob + (double)bin) / (2.0 * kBinScale) - kBinOffset - eps;
             mhi = bin == kBins - 1 ? __builtin_inf() : (double)(bin + 1) / kBinScale - kBinOffset + eps;
         } else {
             materialize(res, M8);

@@ -83,6 +83,30 @@ def make_pair(seed=SEED_BASE, n_features=2000, patch_size=5, width=1241, height=
     return SynthPair(cam, imgs[0], imgs[1], imgs[2], *poses, nr.value, nk.value, px[:n], br[:n], pt[:n], hp[:n])
 
 
+def make_flat_blocks(groups, width=320, height=96, block=12, base=100, fx=300.0):
+    """A pair whose level-0 residuals are chosen exactly: feature i sits on a flat block-by-block square of
+    the ref image (intensity `base`) and of the cur image (intensity base + r_i); identity poses, so every
+    slot of feature i has residual r_i (an integer, bilinear of a flat square).  groups: {r: n_features}.
+    For the robust-scale edge cases of K2 (tests/test_gpu_parity.py); align it on level 0 only."""
+    r = np.repeat(np.array(list(groups.keys()), np.int64), list(groups.values()))
+    n, cols = len(r), width // block - 2
+    assert n <= cols * (height // block - 2) and np.all(np.abs(r) < 64) and 0 <= base + r.min() and base + r.max() <= 255
+    ref = np.full((height, width), 60, np.uint8)
+    cur = ref.copy()
+    px = np.zeros((n, 2))
+    for i in range(n):
+        y0, x0 = block * (1 + i // cols), block * (1 + i % cols)
+        ref[y0:y0 + block, x0:x0 + block] = base
+        cur[y0:y0 + block, x0:x0 + block] = base + r[i]
+        px[i] = (x0 + block / 2 - 0.2, y0 + block / 2 - 0.3)
+    cam = dict(fx=fx, fy=fx, cx=width / 2, cy=height / 2, width=width, height=height)
+    b = np.stack([(px[:, 0] - cam["cx"]) / fx, (px[:, 1] - cam["cy"]) / fx, np.ones(n)], 1)
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    ident = np.array([0, 0, 0, 1, 0, 0, 0], np.float64)
+    return SynthPair(cam, ref.copy(), ref, cur, ident.copy(), ident.copy(), ident.copy(), ident.copy(), n, 0, px, b,
+                     10.0 * b, np.ones(n, np.uint8))
+
+
 def gradient_fraction(img, thr=50):
     img = np.ascontiguousarray(img, np.uint8)
     return lib().svo_synth_gradient_fraction(_p(img), img.shape[1], img.shape[0], thr)

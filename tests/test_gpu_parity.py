@@ -129,6 +129,38 @@ def test_align_edge_cases():
     assert np.abs(canon(p[0]) - canon(pc)).max() <= 1e-9
 
 
+# Residual distributions where rank n/2 is the first element of its bin and the bin below is far away:
+# the even-length median (largest of the lower bin + smallest of the bin) / 2 lies below the median's
+# bin, and K2's MAD bracket must allow for that (found by a model search of K2's bracket; the first
+# case gave MAD 13 instead of 9 before the fix).  Known answers: exact order statistics of the slots.
+FLAT_CASES = [({2: 7, 7: 4, 15: 5, 24: 6}, 11.0, 9.0),
+              ({2: 7, -8: 7, -22: 12, -14: 2}, None, None),
+              ({18: 4, -20: 1, -3: 6, -25: 14, 10: 5}, None, None)]
+
+
+def _exact_med_mad(groups):
+    v = np.sort(np.repeat(np.array(list(groups.keys()), float), [25 * c for c in groups.values()]))
+    m = len(v) // 2
+    med = (v[m - 1] + v[m]) / 2
+    d = np.sort(np.abs(v - med))
+    return med, (d[m - 1] + d[m]) / 2
+
+
+@pytest.mark.parametrize("case", FLAT_CASES)
+def test_align_scale_median_below_its_bin(case):
+    groups, med_known, mad_known = case
+    med_x, mad_x = _exact_med_mad(groups)
+    if med_known is not None:
+        assert (med_x, mad_x) == (med_known, mad_known)
+    s = synth.make_flat_blocks(groups)
+    _, _, _, tr_c = oracle_align(s, 5, 0, 0, mode=1)
+    assert (tr_c[0].median, tr_c[0].mad) == (med_x, mad_x)
+    b, _ = gpu_batch([s], 5, 0, 0)
+    b.run()
+    g = b.traces(0)[0]
+    assert (g.n_vis, g.median, g.mad, g.sigma) == (tr_c[0].n_vis, med_x, mad_x, tr_c[0].sigma)
+
+
 def test_align_no_ref_features():
     s = synth.make_pair(n_features=40)
     s.n_kf, s.n_ref = s.n_ref + s.n_kf, 0

@@ -172,3 +172,14 @@ def test_bilinear_known_answers():
     b = np.float32((1 - x) * 70 + x * 80)
     want = np.float32((2 - y) * np.float64(a) + (y - 1) * np.float64(b))
     assert O.bilinear_f(img, x, y) == want  # float-rounded row blends (src/algorithm.cpp:885-894)
+
+
+def test_oracle_robust_scale_on_flat_blocks():
+    """Exact integer residuals (flat squares, synth.make_flat_blocks): the oracle's level trace holds the
+    exact order statistics, including the even-length median that lies below its histogram bin."""
+    import svo_amd.synth as synth
+    from common import oracle_align
+    for groups, med, mad in [({2: 7, 7: 4, 15: 5, 24: 6}, 11.0, 9.0), ({-5: 3, 5: 3}, 0.0, 5.0)]:
+        s = synth.make_flat_blocks(groups)
+        _, _, _, tr = oracle_align(s, 5, 0, 0, mode=1)
+        assert (tr[0].n_vis, tr[0].median, tr[0].mad) == (25 * sum(groups.values()), med, mad)
