@@ -90,7 +90,7 @@ def make_flat_blocks(groups, width=320, height=96, block=12, base=100, fx=300.0)
     For the robust-scale edge cases of K2 (tests/test_gpu_parity.py); align it on level 0 only."""
     r = np.repeat(np.array(list(groups.keys()), np.int64), list(groups.values()))
     n, cols = len(r), width // block - 2
-    assert n <= cols * (height // block - 2) and np.all(np.abs(r) < 64) and 0 <= base + r.min() and base + r.max() <= 255
+    assert n <= cols * (height // block - 2) and 0 <= base + r.min() and base + r.max() <= 255
     ref = np.full((height, width), 60, np.uint8)
     cur = ref.copy()
     px = np.zeros((n, 2))

@@ -133,17 +133,26 @@ def test_align_edge_cases():
 # the even-length median (largest of the lower bin + smallest of the bin) / 2 lies below the median's
 # bin, and K2's MAD bracket must allow for that (found by a model search of K2's bracket; the first
 # case gave MAD 13 instead of 9 before the fix).  Known answers: exact order statistics of the slots.
+# The other cases drive K2's exact fallbacks: an overfull median bin (> kCandCap slots), overfull MAD
+# candidate bins, the bin below an even-length median holding > kPrevCap slots, an odd length, and
+# outliers past +-64 that clamp into the end bins (MAD 90: its distance bin clamps too).
 FLAT_CASES = [({2: 7, 7: 4, 15: 5, 24: 6}, 11.0, 9.0),
               ({2: 7, -8: 7, -22: 12, -14: 2}, None, None),
-              ({18: 4, -20: 1, -3: 6, -25: 14, 10: 5}, None, None)]
+              ({18: 4, -20: 1, -3: 6, -25: 14, 10: 5}, None, None),
+              ({0: 90, 5: 30, -5: 30}, 0.0, 0.0),
+              ({-3: 50, 3: 50, 0: 2}, 0.0, 3.0),
+              ({1: 20, 4: 20}, 2.5, 1.5),
+              ({1: 3, 2: 2}, 1.0, 0.0),
+              ({-90: 3, 0: 4, 90: 3}, 0.0, 90.0)]
 
 
 def _exact_med_mad(groups):
     v = np.sort(np.repeat(np.array(list(groups.keys()), float), [25 * c for c in groups.values()]))
     m = len(v) // 2
-    med = (v[m - 1] + v[m]) / 2
+    even = len(v) % 2 == 0
+    med = (v[m - 1] + v[m]) / 2 if even else v[m]
     d = np.sort(np.abs(v - med))
-    return med, (d[m - 1] + d[m]) / 2
+    return med, ((d[m - 1] + d[m]) / 2 if even else d[m])
 
 
 @pytest.mark.parametrize("case", FLAT_CASES)
@@ -152,7 +161,7 @@ def test_align_scale_median_below_its_bin(case):
     med_x, mad_x = _exact_med_mad(groups)
     if med_known is not None:
         assert (med_x, mad_x) == (med_known, mad_known)
-    s = synth.make_flat_blocks(groups)
+    s = synth.make_flat_blocks(groups, width=640, height=192)
     _, _, _, tr_c = oracle_align(s, 5, 0, 0, mode=1)
     assert (tr_c[0].median, tr_c[0].mad) == (med_x, mad_x)
     b, _ = gpu_batch([s], 5, 0, 0)
