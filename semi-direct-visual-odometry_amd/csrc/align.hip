@@ -198,10 +198,12 @@ __device__ __forceinline__ void lane_swap(double& x, double& y) {
 
 // 16-bit monotone key of a residual for K2's sweeps: floor((r + 64) * 512) clamped to [0, kKeyMax];
 // 0xFFFF marks an invisible slot.  key >> 4 is exactly the value bin floor((r + 64) * 32) of K2.
+// (r finite.)  fma(r, 512, 32768) rounds exactly like (r + 64) * 512 (scaling by a power of two commutes
+// with rounding): one fma, a clamp at 0, the conversion and a min per pixel.
 __device__ __forceinline__ uint16_t res_key(double r) {
-    if (r == __builtin_inf()) return 0xFFFF;
-    const double t = (r + kBinOffset) * kKeyScale;
-    return (uint16_t)(t < 0.0 ? 0u : (t >= (double)kKeyMax ? kKeyMax : (uint32_t)t));
+    const double t = fmax(fma(r, kKeyScale, kBinOffset * kKeyScale), 0.0);
+    const uint32_t k = (uint32_t)t;
+    return (uint16_t)(k < kKeyMax ? k : kKeyMax);
 }
 
 // XCD-aware workgroup -> (pair, chunk) map for K1 / K3.  Workgroups are dealt round-robin over the
