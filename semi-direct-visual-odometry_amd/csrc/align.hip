@@ -1114,6 +1114,15 @@ __global__ void __launch_bounds__(kSelThreads, 4) align_scale_kernel(AlignArgs a
 }
 // ------------------------------------------------------------------ K3: weights, normal equations, LM step
 namespace {
+// image_jac (src/image_alignment.cpp:194-248) with one reciprocal of z instead of ten divisions: K3's
+// sums are compared within tolerance, and the ulp-level differences are far inside it
+__device__ __forceinline__ void image_jac_rcp(V3 p, double fx, double fy, double a[6], double b[6]) {
+    const double iz = 1.0 / p.z, x = p.x * iz, y = p.y * iz;  // normalised coordinates
+    const double fxi = fx * iz, fyi = fy * iz;
+    a[0] = fxi; a[1] = 0.0; a[2] = -fxi * x; a[3] = -fx * x * y; a[4] = fx * x * x + fx; a[5] = -fx * y;
+    b[0] = 0.0; b[1] = fyi; b[2] = -fyi * y; b[3] = -fy * y * y - fy; b[4] = fy * x * y; b[5] = fy * x;
+}
+
 struct SolveShared {
     double tot[28];
     double A[36];
@@ -1215,7 +1224,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_
     const int f = chunk * kLaneFeats + tid;
     const int W = a.geom.w[level];
     const int64_t loff = a.geom.off[level];
-    const double dom = (double)(1 << level), scale = 1.0 / dom;
+    const double scale = ldexp(1.0, -level);  // exact, no division
     const double c = S.c, inv_c2 = 1.0 / (c * c);
     double acc[32];
 #pragma unroll
@@ -1300,7 +1309,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_
         // a[1] = b[0] = 0).  Per feature sum_px w J J^T = a u^T + b v^T with u = Sxx a + Sxy b,
         // v = Sxy a + Syy b: the 21 lower H terms (row-major lower triangle), the 6 g terms and chi2
         double ja[6], jb[6];
-        image_jac(pw, a.fx / dom, a.fy / dom, ja, jb);
+        image_jac_rcp(pw, a.fx * scale, a.fy * scale, ja, jb);
         double u[6], v[6];
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
