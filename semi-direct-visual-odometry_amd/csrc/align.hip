@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
     if (f0 >= fstride) return;  // whole workgroup
     const int W = a.geom.w[level], H = a.geom.h[level];
     const int64_t loff = a.geom.off[level];
-    const double scale = 1.0 / (double)(1 << level);
+    const double scale = ldexp(1.0, -level);  // = 1 / 2^level exactly, no division
     const int border = h + 2;
     // key of slot (k, f) at keys[k * fstride + f]
     const __amdgpu_buffer_rsrc_t keys = slot_rsrc(a.keys + (int64_t)pair * a.key_stride, a.key_stride * 2);
@@ -895,7 +895,7 @@ __global__ void __launch_bounds__(kSelThreads, 4) align_scale_kernel(AlignArgs a
     res.n_ref = P.n_ref;
     res.half = a.half;
     res.side = 2 * a.half + 1;
-    res.scale = 1.0 / (double)(1 << level);
+    res.scale = ldexp(1.0, -level);
     const uint8_t* __restrict__ fvis = a.fvis + (int64_t)pair * a.max_f;
     K2_STAMP(0, clock64());
     K2_STAMP(14, __builtin_amdgcn_s_memrealtime());  // 100 MHz, chip-wide: workgroup start / end spread
@@ -1284,8 +1284,10 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_
                     const double dx = fma(hfy, D1[kx], hgy * D2[kx]);
                     const double dy = fma(hfy, E0, hgy * E1[kx]);
                     const double r2 = r * r;
-                    const double tt = fma(-r2, inv_c2, 1.0);
-                    const double w = fabs(r) <= c ? tt * tt : 0.0;  // Tukey (src/optimizer.cpp:502-511)
+                    // Tukey (src/optimizer.cpp:502-511): (1 - r^2/c^2)^2 for |r| <= c, else 0, as a clamp
+                    // of the base at 0 (the two forms differ only at |r| = c, by a rounding-sized weight)
+                    const double tt = fmax(fma(-r2, inv_c2, 1.0), 0.0);
+                    const double w = tt * tt;
                     const double wdx = w * dx, wdy = w * dy;
                     sxx = fma(wdx, dx, sxx);
                     sxy = fma(wdx, dy, sxy);
