@@ -47,21 +47,56 @@ constexpr int kPrevCap = 256;        // slots of the bin below the median's gath
 constexpr int kRadixBits = 11;
 constexpr double kDblMax = 1.7976931348623157e308;
 
+// Wave reductions and scans with DPP row operations (GFX9 encodings) instead of shfl (ds_bpermute, an
+// LDS round trip per step): quad_perm / row_half_mirror / row_mirror reduce inside each 16-lane row,
+// readlane combines the four rows.  DPP reads every lane's register regardless of EXEC, so all 64 lanes
+// must be active: every caller is block-uniform code.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const uint2 u = __builtin_bit_cast(uint2, v);
+    return __builtin_bit_cast(double, make_uint2(dpp_mov<kCtrl>(u.x), dpp_mov<kCtrl>(u.y)));
+}
+__device__ __forceinline__ uint32_t lane_read(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ double lane_read(double v, int l) {
+    const uint2 u = __builtin_bit_cast(uint2, v);
+    return __builtin_bit_cast(double, make_uint2(lane_read(u.x, l), lane_read(u.y, l)));
+}
+template <typename T, typename F>
+__device__ __forceinline__ T wave_allreduce(T v, F op) {
+    v = op(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = op(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = op(v, dpp_mov<0x141>(v));  // row_half_mirror
+    v = op(v, dpp_mov<0x140>(v));  // row_mirror: every lane of a row holds the row's result
+    return op(op(lane_read(v, 0), lane_read(v, 16)), op(lane_read(v, 32), lane_read(v, 48)));
+}
 __device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    return v;
+    return wave_allreduce(v, [](uint32_t x, uint32_t y) { return x + y; });
 }
 __device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_down(v, o, 64));
-    return __shfl(v, 0, 64);
+    return wave_allreduce(v, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
 }
 __device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_down(v, o, 64));
-    return __shfl(v, 0, 64);
+    return wave_allreduce(v, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
 }
 __device__ __forceinline__ double wave_max(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_down(v, o, 64));
-    return v;
+    return wave_allreduce(v, [](double x, double y) { return fmax(x, y); });
+}
+// inclusive prefix sum over the wave: row_shr 1..3 (bound_ctrl zero-fills across the row start), row_shr
+// 4 / 8 into banks 1-3 / 2-3, then row_bcast 15 / 31 carry the row totals into rows 1, 3 / 2, 3
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    uint32_t s = v;
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xF, 0xF, true);
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x114, 0xF, 0xE, true);
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x118, 0xF, 0xC, true);
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xA, 0xF, false);
+    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xC, 0xF, false);
+    return s;
 }
 
 // Window geometry of one feature at one level (patch half size kHalf), in image cells relative to
@@ -621,11 +656,7 @@ __device__ void find_bin(SelShared& sh, const uint32_t* hist, int bins) {
         const int b = tid * per + i;
         if (b < bins) local += hist[b];
     }
-    uint32_t incl = local;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-    }
+    uint32_t incl = wave_incl_scan(local);
     if (lane == 63) sh.scan[wave] = incl;
     __syncthreads();
     uint32_t off = 0;
@@ -696,7 +727,7 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
     const int leader = __ffsll((unsigned long long)m) - 1;
     uint32_t base = 0;
     if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
-    base = __shfl(base, leader, 64);
+    base = lane_read(base, leader);
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
 }
 
