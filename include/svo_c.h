@@ -162,6 +162,37 @@ int svo_feature_align(svo_ctx* ctx, const svo_camera* cam, int32_t patch_size, c
                       const int32_t* ref_frames, int32_t ref_frame, const svo_pyramid_set* cur_set, int32_t cur_frame,
                       int32_t n, const double* ref_px, double* px_inout, double* err, int32_t* status);
 
+/* As svo_feature_align, with each candidate's reference frame in a pyramid set of its own:
+ * candidate i reads ref_sets[i] frame ref_frames[i] (the batched call Map::reprojectCell and
+ * Map::addCandidateToFrame make: their candidates come from different keyframes). */
+int svo_feature_align_multi(svo_ctx* ctx, const svo_camera* cam, int32_t patch_size, const svo_pyramid_set* const* ref_sets,
+                            const int32_t* ref_frames, const svo_pyramid_set* cur_set, int32_t cur_frame, int32_t n,
+                            const double* ref_px, double* px_inout, double* err, int32_t* status);
+
+/* ---------------------------------------------------------------- map reprojection (host side)
+ * Frame::world2image (src/frame.cpp:83-92): px[i] = project2d(pose * points[i]) for n points (n x 3). */
+int svo_world2image(const svo_camera* cam, const double* pose, int32_t n, const double* points, double* px);
+
+/* The decisions of Map::reprojectMap (src/map.cpp:260-267, 436-478) with reprojectPoint (:481-492) and
+ * reprojectCell (:495-570), before any FeatureAlignment: the reference accepts the aligned position of
+ * the first non-deleted candidate of a cell whatever its error, so which candidates are aligned is fixed
+ * by the geometry alone and the alignments can run as one batch (svo_feature_align_multi).
+ * Grid: cell_size-pixel cells, n_cells = ceil(W / c) * ceil(H / c), visited in cell_order (the
+ * reference shuffles it with an unseeded std::random_device; callers pass a seeded permutation).
+ * Keyframes k < n_kf (ref frame, then its last keyframe) own features kf_feat_off[k] .. kf_feat_off[k+1]-1;
+ * feat_point[f] is the feature's point (-1: none).  Points: position (n_points x 3), type
+ * (Point::PointType: 0 GOOD, 1 DELETED, 2 CANDIDATE, 3 UNKNOWN), point_last = m_lastProjectedKFId
+ * (updated: set to cur_id for every point projected).  Out: overlap[k] points of keyframe k in the
+ * frame; the selected candidates in acceptance order (sel_feat, sel_cell, sel_px = the initial
+ * pixel for the alignment; capacity n_cells); matches (m_matches) and trials (m_trials).  The caller
+ * applies the per-candidate effects (:558-569): succeededProjection += 1, UNKNOWN -> GOOD past 10, a new
+ * feature at the aligned pixel, and marks sel_cell visited. */
+int svo_map_reproject_plan(const svo_camera* cam, int32_t cell_size, int32_t n_cells, const int32_t* cell_order,
+                           const double* cur_pose, uint64_t cur_id, int32_t n_kf, const int32_t* kf_feat_off,
+                           const int32_t* feat_point, int32_t n_points, const double* point_pos,
+                           const uint32_t* point_type, uint64_t* point_last, int32_t* overlap, int32_t* n_sel,
+                           int32_t* sel_feat, int32_t* sel_cell, double* sel_px, int32_t* matches, int32_t* trials);
+
 /* ---------------------------------------------------------------- depth filter
  * One depth-filter seed: MixedGaussianFilter (include/mixed_gaussian_filter.hpp:28-38) and the feature
  * it refines (m_feature: pixel position and bearing in its keyframe). */

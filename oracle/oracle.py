@@ -265,3 +265,51 @@ def depth_triangulate(rel_pose, f_ref, f_cur):
     r, a, b = (np.ascontiguousarray(x, np.float64) for x in (rel_pose, f_ref, f_cur))
     ok = lib().oracle_depth_triangulate(_p(r), _p(a), _p(b), ctypes.byref(d))
     return bool(ok), d.value
+
+
+def reproject_map(cam, cell_size, cell_order, cur_pose, cur_id, cur_grad, kf_grads, kf_feat_off, feat_px, feat_point,
+                  point_pos, point_type, point_succ, point_last, cell_visited):
+    """Map::reprojectMap (src/map.cpp:260-570) restated with one FeatureAlignment call per accepted candidate.
+    point_type / point_succ / point_last / cell_visited are updated in place.  Returns (overlap, new_px,
+    new_point, new_feat, matches, trials)."""
+    n_kf = len(kf_grads)
+    grads = [np.ascontiguousarray(g, np.uint8) for g in kf_grads]
+    gp = (ctypes.c_void_p * n_kf)(*[g.ctypes.data for g in grads])
+    cg = np.ascontiguousarray(cur_grad, np.uint8)
+    n_cells = len(cell_order)
+    overlap = np.zeros(n_kf, np.int32)
+    new_px = np.zeros((n_cells, 2))
+    new_point = np.zeros(n_cells, np.int32)
+    new_feat = np.zeros(n_cells, np.int32)
+    nn, m, t = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    c = camera(cam)
+    args = [np.ascontiguousarray(a, dt) for a, dt in ((cell_order, np.int32), (cur_pose, np.float64),
+                                                     (kf_feat_off, np.int32), (feat_px, np.float64),
+                                                     (feat_point, np.int32), (point_pos, np.float64))]
+    for a, dt in ((point_type, np.uint32), (point_succ, np.uint32), (point_last, np.uint64), (cell_visited, np.uint8)):
+        assert a.dtype == dt and a.flags.c_contiguous
+    lib().oracle_reproject_map(ctypes.byref(c), int(cell_size), _p(args[0]), _p(args[1]), ctypes.c_uint64(cur_id),
+                               _p(cg), n_kf, gp, _p(args[2]), _p(args[3]), _p(args[4]), _p(args[5]),
+                               _p(point_type), _p(point_succ), _p(point_last), _p(cell_visited), _p(overlap),
+                               ctypes.byref(nn), _p(new_px), _p(new_point), _p(new_feat), ctypes.byref(m),
+                               ctypes.byref(t))
+    k = nn.value
+    return overlap, new_px[:k], new_point[:k], new_feat[:k], m.value, t.value
+
+
+def add_candidates(cam, cell_size, cell_visited, cur_pose, cur_grad, cand_grads, cand_px, cand_point_pos):
+    """Map::addCandidateToFrame (src/map.cpp:595-627) restated sequentially.  cell_visited is updated in
+    place.  Returns (matched, new_px)."""
+    n = len(cand_grads)
+    grads = [np.ascontiguousarray(g, np.uint8) for g in cand_grads]
+    gp = (ctypes.c_void_p * max(n, 1))(*[g.ctypes.data for g in grads])
+    matched = np.zeros(max(n, 1), np.uint8)
+    new_px = np.zeros((max(n, 1), 2))
+    assert cell_visited.dtype == np.uint8 and cell_visited.flags.c_contiguous
+    c = camera(cam)
+    cpx = np.ascontiguousarray(cand_px, np.float64)
+    cpp = np.ascontiguousarray(cand_point_pos, np.float64)
+    lib().oracle_add_candidates(ctypes.byref(c), int(cell_size), _p(cell_visited),
+                                _p(np.ascontiguousarray(cur_pose, np.float64)), _p(np.ascontiguousarray(cur_grad, np.uint8)),
+                                n, gp, _p(cpx), _p(cpp), _p(matched), _p(new_px))
+    return matched[:n].astype(bool), new_px[:n]

@@ -1072,4 +1072,101 @@ int32_t oracle_depth_triangulate(const double* rel7, const double* fref, const d
     return depth_from_triangulation(rel, {fref[0], fref[1], fref[2]}, {fcur[0], fcur[1], fcur[2]}, *depth) ? 1 : 0;
 }
 
+// ---------------------------------------------------------------- Map reprojection (src/map.cpp)
+// Map::reprojectMap (:260-478) with reprojectPoint (:481-492) and reprojectCell (:495-570), restated
+// sequentially: one FeatureAlignment(7, 0, 3) call per accepted candidate, in the reference's order.
+// Keyframe k (ref frame, then its last keyframe) owns features kf_feat_off[k] .. kf_feat_off[k+1]-1 at
+// feat_px, observing point feat_point (-1: none).  Point state in/out: type (0 GOOD, 1 DELETED,
+// 2 CANDIDATE, 3 UNKNOWN), succeeded projections, last projected frame id.  cell_visited (in/out) is the
+// Map's m_cellVisited.  Out: overlap per keyframe, the new features of cur (aligned pixel, point,
+// source feature) in creation order, m_matches, m_trials.
+void oracle_reproject_map(const oc_camera* c, int32_t cell_size, const int32_t* cell_order, const double* cur_pose,
+                          uint64_t cur_id, const uint8_t* cur_grad, int32_t n_kf, const uint8_t* const* kf_grad,
+                          const int32_t* kf_feat_off, const double* feat_px, const int32_t* feat_point,
+                          const double* point_pos, uint32_t* point_type, uint32_t* point_succ, uint64_t* point_last,
+                          uint8_t* cell_visited, int32_t* overlap, int32_t* n_new, double* new_px, int32_t* new_point,
+                          int32_t* new_feat, int32_t* matches, int32_t* trials) {
+    const Camera cam{c->fx, c->fy, c->cx, c->cy, c->width, c->height};
+    const SE3 T{{cur_pose[0], cur_pose[1], cur_pose[2], cur_pose[3]}, {cur_pose[4], cur_pose[5], cur_pose[6]}};
+    const uint32_t cols = (uint32_t)std::ceil((double)c->width / cell_size), rows = (uint32_t)std::ceil((double)c->height / cell_size);
+    struct Cand { int32_t feat, kf, point; };
+    std::vector<std::vector<Cand>> cells(cols * rows);  // resetGrid (:250-258)
+    int32_t m = 0, t = 0, nn = 0;
+    auto world2image = [&](int32_t p) { return cam.project2d(act(T, {point_pos[3 * p], point_pos[3 * p + 1], point_pos[3 * p + 2]})); };
+    for (int32_t k = 0; k < n_kf; ++k) {
+        overlap[k] = 0;
+        for (int32_t f = kf_feat_off[k]; f < kf_feat_off[k + 1]; ++f) {
+            const int32_t p = feat_point[f];
+            if (p < 0) continue;                 // feature->m_point == nullptr
+            if (point_last[p] == cur_id) continue;
+            point_last[p] = cur_id;
+            const V2 px = world2image(p);        // reprojectPoint
+            if (!cam.is_in_frame(px, 3)) continue;
+            const int32_t cell = (int32_t)((uint32_t)(int32_t)px.y / (uint32_t)cell_size * cols + (uint32_t)(int32_t)px.x / (uint32_t)cell_size);
+            cells[cell].push_back({f, k, p});
+            ++overlap[k];
+        }
+    }
+    FeatureAlignment fa(7, &cam);
+    const Image cg{cur_grad, c->width, c->height};
+    for (uint32_t i = 0; i < cells.size(); ++i) {
+        const int32_t idx = cell_order[i];
+        std::vector<Cand>& cand = cells[idx];
+        bool accepted = false;
+        if (!cand.empty()) {  // reprojectCell
+            std::sort(cand.begin(), cand.end(), [&](const Cand& a, const Cand& b) { return point_type[a.point] > point_type[b.point]; });
+            for (const Cand& cd : cand) {
+                ++t;
+                if (point_type[cd.point] == 1u) continue;  // DELETED
+                V2 px = world2image(cd.point);
+                int32_t st = 0;
+                (void)fa.align({kf_grad[cd.kf], c->width, c->height}, {feat_px[2 * cd.feat], feat_px[2 * cd.feat + 1]}, cg, px, &st);
+                ++point_succ[cd.point];
+                if (point_type[cd.point] == 3u && point_succ[cd.point] > 10) point_type[cd.point] = 0u;  // UNKNOWN -> GOOD
+                new_px[2 * nn] = px.x; new_px[2 * nn + 1] = px.y;
+                new_point[nn] = cd.point;
+                new_feat[nn] = cd.feat;
+                ++nn;
+                accepted = true;
+                break;
+            }
+        }
+        if (accepted) {
+            ++m;
+            cell_visited[idx] = 1;
+        }
+        if (m > 150) break;
+    }
+    *n_new = nn;
+    *matches = m;
+    *trials = t;
+}
+
+// Map::addCandidateToFrame (src/map.cpp:595-627) restated sequentially over the candidate list:
+// candidate i = (its feature: gradient of its frame cand_grad[i] at cand_px[i]; its point at
+// cand_point_pos[i]).  matched[i] = 1 and new_px[i] = the aligned pixel when it was added.
+void oracle_add_candidates(const oc_camera* c, int32_t cell_size, uint8_t* cell_visited, const double* cur_pose,
+                           const uint8_t* cur_grad, int32_t n_cand, const uint8_t* const* cand_grad,
+                           const double* cand_px, const double* cand_point_pos, uint8_t* matched, double* new_px) {
+    const Camera cam{c->fx, c->fy, c->cx, c->cy, c->width, c->height};
+    const SE3 T{{cur_pose[0], cur_pose[1], cur_pose[2], cur_pose[3]}, {cur_pose[4], cur_pose[5], cur_pose[6]}};
+    const uint32_t cols = (uint32_t)std::ceil((double)c->width / cell_size);
+    FeatureAlignment fa(7, &cam);
+    const Image cg{cur_grad, c->width, c->height};
+    for (int32_t i = 0; i < n_cand; ++i) {
+        matched[i] = 0;
+        V2 px = cam.project2d(act(T, {cand_point_pos[3 * i], cand_point_pos[3 * i + 1], cand_point_pos[3 * i + 2]}));
+        if (!cam.is_in_frame(px, 3)) continue;
+        const int32_t k = (int32_t)((uint32_t)(int32_t)px.y / (uint32_t)cell_size * cols + (uint32_t)(int32_t)px.x / (uint32_t)cell_size);
+        if (cell_visited[k]) continue;
+        int32_t st = 0;
+        const double err = fa.align({cand_grad[i], c->width, c->height}, {cand_px[2 * i], cand_px[2 * i + 1]}, cg, px, &st);
+        if (err < 50.0) {
+            matched[i] = 1;
+            new_px[2 * i] = px.x; new_px[2 * i + 1] = px.y;
+            cell_visited[k] = 1;
+        }
+    }
+}
+
 }  // extern "C"

@@ -76,6 +76,12 @@ _SIGNATURES = [
     ("svo_align_batch_traces", c_int32, [c_void_p, c_int32, c_void_p]),
     ("svo_feature_align", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_int32,
                                     c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("svo_feature_align_multi", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_void_p,
+                                          c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("svo_world2image", c_int32, [ctypes.POINTER(SvoCamera), c_void_p, c_int32, c_void_p, c_void_p]),
+    ("svo_map_reproject_plan", c_int32, [ctypes.POINTER(SvoCamera), c_int32, c_int32, c_void_p, c_void_p,
+                                         ctypes.c_uint64, c_int32, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, P_i32, c_void_p, c_void_p, c_void_p, P_i32, P_i32]),
     ("svo_depth_seed_init", c_int32, [c_double, c_double, c_void_p]),
     ("svo_depth_update", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_int32, c_void_p, c_int32, c_void_p, P_i32, c_void_p, c_void_p,

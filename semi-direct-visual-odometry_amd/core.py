@@ -188,9 +188,28 @@ class ImagePyramid:
         self.set = None
 
 
+class PointType:  # Point::PointType (include/point.hpp:18-24)
+    GOOD, DELETED, CANDIDATE, UNKNOWN = 0, 1, 2, 3
+
+
 class Point:
+    """Point(position) (src/point.cpp:6-18): position, type, the observing features and the
+    reprojection bookkeeping the Map reads (include/point.hpp:28-40)."""
+    NO_FRAME = 2 ** 64 - 1  # m_lastProjectedKFId(-1) on a uint64
+
     def __init__(self, position):
         self.position = np.asarray(position, dtype=np.float64)
+        self.type = PointType.UNKNOWN
+        self.features = []
+        self.last_projected_kf_id = Point.NO_FRAME
+        self.failed_projection = 0
+        self.succeeded_projection = 0
+
+    def add_feature(self, feature):  # src/point.cpp:35-38
+        self.features.append(feature)
+
+    def find_frame(self, frame):  # src/point.cpp: any observing feature in `frame`
+        return any(f.frame is frame for f in self.features)
 
 
 class Feature:
@@ -211,6 +230,8 @@ class Feature:
 class Frame:
     """Frame(camera, img, maxImagePyramid, timestamp, lastKeyframe) (src/frame.cpp:6-27)."""
 
+    _frame_counter = 0  # Frame::m_frameCounter
+
     def __init__(self, camera, image, max_image_pyramid, timestamp=0, last_keyframe=None, ctx=None):
         img = np.asarray(image)
         if img.dtype != np.uint8 or img.ndim != 2 or img.shape != (camera.height, camera.width):
@@ -221,6 +242,17 @@ class Frame:
         self.features = []
         self.last_keyframe = last_keyframe
         self.timestamp = timestamp
+        self.id = Frame._frame_counter
+        Frame._frame_counter += 1
+
+    def world2image(self, points):
+        """Frame::world2image (src/frame.cpp:83-92) for an (n, 3) array (or one point)."""
+        pts = np.ascontiguousarray(np.atleast_2d(points), dtype=np.float64)
+        out = np.zeros((pts.shape[0], 2))
+        cam = self.camera.as_c()
+        check(lib().svo_world2image(ctypes.byref(cam), ptr(np.ascontiguousarray(self.abs_pose, np.float64)),
+                                    pts.shape[0], ptr(pts), ptr(out)))
+        return out if np.ndim(points) == 2 else out[0]
 
     def add_feature(self, feature):
         self.features.append(feature)
@@ -377,6 +409,142 @@ class FeatureAlignment:
         check(lib().svo_feature_align(self.ctx.handle, ctypes.byref(cam), self.patch_size, ref_set.handle, ptr(rf), 0,
                                       cur_set.handle, int(cur_frame), n, ptr(ref_px), ptr(px_inout), ptr(err), ptr(st)))
         return err, st
+
+
+    def align_many(self, ref_features, cur_frame, px_inout):
+        """align() for every (ref_features[i], px_inout[i]) against cur_frame in one launch; each
+        reference feature reads the gradient of its own frame (svo_feature_align_multi)."""
+        n = len(ref_features)
+        if px_inout.dtype != np.float64 or not px_inout.flags.c_contiguous or px_inout.shape != (n, 2):
+            raise ValueError("px_inout must be a C-contiguous float64 (n, 2) array")
+        err = np.zeros(n)
+        st = np.zeros(n, np.int32)
+        if n == 0:
+            return err, st
+        sets = (ctypes.c_void_p * n)(*[f.frame.image_pyramid.set.handle.value for f in ref_features])
+        frames = np.zeros(n, np.int32)
+        ref_px = np.ascontiguousarray([f.pixel_position for f in ref_features], dtype=np.float64)
+        cam = cur_frame.camera.as_c()
+        check(lib().svo_feature_align_multi(self.ctx.handle, ctypes.byref(cam), self.patch_size, sets, ptr(frames),
+                                            cur_frame.image_pyramid.set.handle, 0, n, ptr(ref_px), ptr(px_inout),
+                                            ptr(err), ptr(st)))
+        return err, st
+
+
+# ---------------------------------------------------------------- map reprojection
+class Map:
+    """Map(camera, cellSize) (src/map.cpp:15-19; grid :222-248): the reprojection half of the reference's
+    map, reprojectMap (:260-478) with reprojectPoint (:481-492) and reprojectCell (:495-570),
+    addNewCandidate (:586-593), addCandidateToFrame (:595-627) and removeMatchedCandidate (:629-634).
+
+    The reference aligns candidates one FeatureAlignment(7, 0, 3) call at a time; here every alignment of
+    a call runs in one launch (svo_feature_align_multi) and the decisions are replayed in the reference's
+    order: reprojectCell accepts the first non-deleted candidate of a cell whatever its error, so the
+    aligned set is fixed before the alignment (svo_map_reproject_plan); addCandidateToFrame aligns every
+    candidate whose cell is free and then lets the first match of each cell win.  The cell order is a
+    seeded permutation (the reference shuffles it with an unseeded std::random_device, :243-247)."""
+
+    MAX_MATCHES = 150  # :474
+
+    def __init__(self, camera, cell_size, seed=0, ctx=None):
+        self.camera = camera
+        self.cell_size = int(cell_size)
+        self.grid_cols = int(math.ceil(camera.width / self.cell_size))
+        self.grid_rows = int(math.ceil(camera.height / self.cell_size))
+        n = self.grid_cols * self.grid_rows
+        self.cell_orders = np.random.default_rng(seed).permutation(n).astype(np.int32)
+        self.cell_visited = np.zeros(n, bool)  # never cleared by the reference (resetGrid :250-258)
+        self.matches = 0
+        self.trials = 0
+        self.candidates = []  # [feature, point, matched]
+        self.alignment = FeatureAlignment(7, 0, 3, ctx)
+        self.key_frames = []
+
+    def cell_of(self, px):
+        return int(px[1]) // self.cell_size * self.grid_cols + int(px[0]) // self.cell_size
+
+    def reproject_map(self, ref_frame, cur_frame, overlap_keyframes):
+        if ref_frame.last_keyframe is None:
+            raise ValueError("reprojectMap needs refFrame->m_lastKeyframe")
+        kfs = [ref_frame, ref_frame.last_keyframe]
+        feats = [f for kf in kfs for f in kf.features]
+        off = np.cumsum([0] + [len(kf.features) for kf in kfs]).astype(np.int32)
+        index, points = {}, []
+        feat_point = np.full(max(len(feats), 1), -1, np.int32)
+        for i, f in enumerate(feats):
+            if f.point is not None:
+                k = index.setdefault(id(f.point), len(points))
+                if k == len(points):
+                    points.append(f.point)
+                feat_point[i] = k
+        npt = len(points)
+        pos = np.ascontiguousarray([p.position for p in points] or np.zeros((1, 3)), dtype=np.float64)
+        ptype = np.array([p.type for p in points] or [0], np.uint32)
+        plast = np.array([p.last_projected_kf_id for p in points] or [0], np.uint64)
+        n_cells = len(self.cell_orders)
+        overlap = np.zeros(len(kfs), np.int32)
+        sel_feat = np.zeros(n_cells, np.int32)
+        sel_cell = np.zeros(n_cells, np.int32)
+        sel_px = np.zeros((n_cells, 2))
+        n_sel, m, t = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        cam = self.camera.as_c()
+        check(lib().svo_map_reproject_plan(ctypes.byref(cam), self.cell_size, n_cells, ptr(self.cell_orders),
+                                           ptr(np.ascontiguousarray(cur_frame.abs_pose, np.float64)),
+                                           ctypes.c_uint64(cur_frame.id), len(kfs), ptr(off), ptr(feat_point), npt,
+                                           ptr(pos), ptr(ptype), ptr(plast), ptr(overlap), ctypes.byref(n_sel),
+                                           ptr(sel_feat), ptr(sel_cell), ptr(sel_px), ctypes.byref(m),
+                                           ctypes.byref(t)))
+        for p, last in zip(points, plast):
+            p.last_projected_kf_id = int(last)
+        for k, kf in enumerate(kfs):
+            overlap_keyframes.append((kf, int(overlap[k])))
+        self.matches, self.trials = m.value, t.value
+        ns = n_sel.value
+        chosen = [feats[i] for i in sel_feat[:ns]]
+        px = np.ascontiguousarray(sel_px[:ns])
+        self.alignment.align_many(chosen, cur_frame, px)
+        for i, ref_feature in enumerate(chosen):  # :558-569
+            point = ref_feature.point
+            point.succeeded_projection += 1
+            if point.type == PointType.UNKNOWN and point.succeeded_projection > 10:
+                point.type = PointType.GOOD
+            feature = Feature(cur_frame, px[i].copy(), 0)
+            cur_frame.add_feature(feature)
+            feature.set_point(point)
+            point.add_feature(feature)
+            self.cell_visited[sel_cell[i]] = True
+
+    def add_new_candidate(self, feature, point, matched=False):
+        point.type = PointType.CANDIDATE
+        self.candidates.append([feature, point, matched])
+
+    def add_candidate_to_frame(self, frame):
+        if not self.candidates:
+            return
+        px0 = frame.world2image(np.array([c[1].position for c in self.candidates]))
+        w, h = frame.camera.width, frame.camera.height
+        elig, cells = [], []
+        for i, q in enumerate(px0):
+            if q[0] >= 3 and q[1] >= 3 and q[0] < w - 3 and q[1] < h - 3:
+                k = self.cell_of(q)
+                if not self.cell_visited[k]:
+                    elig.append(i)
+                    cells.append(k)
+        px = np.ascontiguousarray(px0[elig])
+        err, _ = self.alignment.align_many([self.candidates[i][0] for i in elig], frame, px)
+        for j, i in enumerate(elig):  # the reference's order: a cell taken earlier in this loop is skipped
+            if self.cell_visited[cells[j]] or not err[j] < 50.0:
+                continue
+            feat, point = self.candidates[i][0], self.candidates[i][1]
+            feature = Feature(frame, px[j].copy(), 0)
+            frame.add_feature(feature)
+            point.add_feature(feat)
+            point.add_feature(feature)
+            feat.set_point(point)
+            feature.set_point(point)
+            self.candidates[i][2] = True
+            self.cell_visited[cells[j]] = True
+        self.candidates = [c for c in self.candidates if not c[2]]  # removeMatchedCandidate
 
 
 # ---------------------------------------------------------------- depth filter

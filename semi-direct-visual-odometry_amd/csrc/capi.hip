@@ -1,6 +1,7 @@
 // capi.hip — the C ABI (include/svo_c.h): contexts, device-resident pyramid sets, alignment batches.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -11,6 +12,7 @@
 #include <vector>
 
 #include "svo_internal.h"
+#include "svo_math.h"
 
 namespace {
 
@@ -509,25 +511,10 @@ int svo_align_batch_traces(svo_align_batch* b, int32_t pair, svo_level_trace* ou
 }
 
 // ------------------------------------------------------------------ feature alignment
-int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, const svo_pyramid_set* ref_set,
-                      const int32_t* ref_frames, int32_t ref_frame, const svo_pyramid_set* cur_set, int32_t cur_frame,
-                      int32_t n, const double* ref_px, double* px_inout, double* err, int32_t* status) {
-    if (!c || !cam || !ref_set || !cur_set || (n > 0 && (!ref_px || !px_inout))) return fail(SVO_ERR_ARG, "null argument");
-    if (n < 0) return fail(SVO_ERR_ARG, "n < 0");
-    if (patch_size < 1 || (2 * (patch_size / 2) + 1) * (2 * (patch_size / 2) + 1) > 128)
-        return fail(SVO_ERR_ARG, "patch_size %d unsupported (footprint must be <= 128 px)", patch_size);
-    for (const svo_pyramid_set* p : {ref_set, cur_set}) {
-        if (p->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
-        if (p->width != cam->width || p->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
-    }
-    if (cur_frame < 0 || cur_frame >= cur_set->n_frames) return fail(SVO_ERR_ARG, "cur_frame out of range");
-    if (n == 0) return SVO_OK;
-    std::vector<const uint8_t*> rg(n);
-    for (int32_t i = 0; i < n; ++i) {
-        const int32_t f = ref_frames ? ref_frames[i] : ref_frame;
-        if (f < 0 || f >= ref_set->n_frames) return fail(SVO_ERR_ARG, "ref frame %d out of range", f);
-        rg[i] = ref_set->d_base + (size_t)f * ref_set->stride + ref_set->grad_off;
-    }
+// One FeatureAlignment launch over n candidates whose reference gradient planes are rg[i].
+static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_size, const std::vector<const uint8_t*>& rg,
+                              const svo_pyramid_set* cur_set, int32_t cur_frame, int32_t n, const double* ref_px,
+                              double* px_inout, double* err, int32_t* status) {
     SVO_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const uint8_t** d_rg = nullptr;
@@ -564,6 +551,134 @@ int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, con
     for (void* p : {(void*)d_rg, (void*)d_st, (void*)d_rpx, (void*)d_px, (void*)d_err})
         if (p) (void)hipFree(p);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
+    return SVO_OK;
+}
+
+static int feature_align_check(svo_ctx* c, const svo_camera* cam, int32_t patch_size, const svo_pyramid_set* cur_set,
+                               int32_t cur_frame, int32_t n, const double* ref_px, const double* px_inout) {
+    if (!c || !cam || !cur_set || (n > 0 && (!ref_px || !px_inout))) return fail(SVO_ERR_ARG, "null argument");
+    if (n < 0) return fail(SVO_ERR_ARG, "n < 0");
+    if (patch_size < 1 || (2 * (patch_size / 2) + 1) * (2 * (patch_size / 2) + 1) > 128)
+        return fail(SVO_ERR_ARG, "patch_size %d unsupported (footprint must be <= 128 px)", patch_size);
+    if (cur_set->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
+    if (cur_set->width != cam->width || cur_set->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
+    if (cur_frame < 0 || cur_frame >= cur_set->n_frames) return fail(SVO_ERR_ARG, "cur_frame out of range");
+    return SVO_OK;
+}
+
+int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, const svo_pyramid_set* ref_set,
+                      const int32_t* ref_frames, int32_t ref_frame, const svo_pyramid_set* cur_set, int32_t cur_frame,
+                      int32_t n, const double* ref_px, double* px_inout, double* err, int32_t* status) {
+    if (int r = feature_align_check(c, cam, patch_size, cur_set, cur_frame, n, ref_px, px_inout)) return r;
+    if (!ref_set) return fail(SVO_ERR_ARG, "null argument");
+    if (ref_set->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
+    if (ref_set->width != cam->width || ref_set->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
+    if (n == 0) return SVO_OK;
+    std::vector<const uint8_t*> rg(n);
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t f = ref_frames ? ref_frames[i] : ref_frame;
+        if (f < 0 || f >= ref_set->n_frames) return fail(SVO_ERR_ARG, "ref frame %d out of range", f);
+        rg[i] = ref_set->d_base + (size_t)f * ref_set->stride + ref_set->grad_off;
+    }
+    return feature_align_impl(c, cam, patch_size, rg, cur_set, cur_frame, n, ref_px, px_inout, err, status);
+}
+
+int svo_feature_align_multi(svo_ctx* c, const svo_camera* cam, int32_t patch_size, const svo_pyramid_set* const* ref_sets,
+                            const int32_t* ref_frames, const svo_pyramid_set* cur_set, int32_t cur_frame, int32_t n,
+                            const double* ref_px, double* px_inout, double* err, int32_t* status) {
+    if (int r = feature_align_check(c, cam, patch_size, cur_set, cur_frame, n, ref_px, px_inout)) return r;
+    if (n > 0 && (!ref_sets || !ref_frames)) return fail(SVO_ERR_ARG, "null argument");
+    if (n == 0) return SVO_OK;
+    std::vector<const uint8_t*> rg(n);
+    for (int32_t i = 0; i < n; ++i) {
+        const svo_pyramid_set* p = ref_sets[i];
+        if (!p) return fail(SVO_ERR_ARG, "candidate %d: null pyramid set", i);
+        if (p->ctx != c) return fail(SVO_ERR_ARG, "candidate %d: pyramid set belongs to another context", i);
+        if (p->width != cam->width || p->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
+        if (ref_frames[i] < 0 || ref_frames[i] >= p->n_frames) return fail(SVO_ERR_ARG, "ref frame %d out of range", ref_frames[i]);
+        rg[i] = p->d_base + (size_t)ref_frames[i] * p->stride + p->grad_off;
+    }
+    return feature_align_impl(c, cam, patch_size, rg, cur_set, cur_frame, n, ref_px, px_inout, err, status);
+}
+
+// ------------------------------------------------------------------ map reprojection (host planning)
+// Frame::world2image (src/frame.cpp:83-92) with PinholeCamera::project2d (src/pinhole_camera.cpp:53-57):
+// the same arithmetic, in the same order, as the device and oracle paths (no FMA contraction).
+static inline void world2image(const svo_camera* cam, const svo::SE3& T, const double* p, double* px) {
+    const svo::V3 c = svo::se3_act(T, svo::V3{p[0], p[1], p[2]});
+    px[0] = cam->fx * (c.x / c.z) + cam->cx;
+    px[1] = cam->fy * (c.y / c.z) + cam->cy;
+}
+static inline bool in_frame(const svo_camera* cam, const double* px, double b) {  // src/pinhole_camera.cpp:163-168
+    return px[0] >= b && px[1] >= b && px[0] < cam->width - b && px[1] < cam->height - b;
+}
+
+int svo_world2image(const svo_camera* cam, const double* pose, int32_t n, const double* points, double* px) {
+    if (!cam || !pose || n < 0 || (n > 0 && (!points || !px))) return fail(SVO_ERR_ARG, "null argument");
+    const svo::SE3 T = svo::se3_load(pose);
+    for (int32_t i = 0; i < n; ++i) world2image(cam, T, points + 3 * i, px + 2 * i);
+    return SVO_OK;
+}
+
+int svo_map_reproject_plan(const svo_camera* cam, int32_t cell_size, int32_t n_cells, const int32_t* cell_order,
+                           const double* cur_pose, uint64_t cur_id, int32_t n_kf, const int32_t* kf_feat_off,
+                           const int32_t* feat_point, int32_t n_points, const double* point_pos,
+                           const uint32_t* point_type, uint64_t* point_last, int32_t* overlap, int32_t* n_sel,
+                           int32_t* sel_feat, int32_t* sel_cell, double* sel_px, int32_t* matches, int32_t* trials) {
+    if (!cam || !cell_order || !cur_pose || !kf_feat_off || !overlap || !n_sel || !sel_feat || !sel_cell || !sel_px ||
+        !matches || !trials || (n_points > 0 && (!point_pos || !point_type || !point_last)))
+        return fail(SVO_ERR_ARG, "null argument");
+    if (cell_size < 1) return fail(SVO_ERR_ARG, "cell_size %d", cell_size);
+    const int32_t cols = (int32_t)std::ceil((double)cam->width / cell_size);  // src/map.cpp:226-227
+    const int32_t rows = (int32_t)std::ceil((double)cam->height / cell_size);
+    if (n_cells != cols * rows) return fail(SVO_ERR_ARG, "n_cells %d != %d x %d", n_cells, cols, rows);
+    if (n_kf < 0 || (kf_feat_off[n_kf] > 0 && !feat_point)) return fail(SVO_ERR_ARG, "bad feature table");
+    for (int32_t i = 0; i < n_cells; ++i)
+        if (cell_order[i] < 0 || cell_order[i] >= n_cells) return fail(SVO_ERR_ARG, "cell_order[%d] out of range", i);
+    const svo::SE3 T = svo::se3_load(cur_pose);
+    std::vector<std::vector<int32_t>> cells(n_cells);  // resetGrid (:250-258)
+    double px[2];
+    for (int32_t k = 0; k < n_kf; ++k) {  // closeKeyframes: ref, then ref->lastKeyframe (:441-461)
+        overlap[k] = 0;
+        for (int32_t f = kf_feat_off[k]; f < kf_feat_off[k + 1]; ++f) {
+            const int32_t p = feat_point[f];
+            if (p < 0) continue;
+            if (p >= n_points) return fail(SVO_ERR_ARG, "feature %d: point %d out of range", f, p);
+            if (point_last[p] == cur_id) continue;
+            point_last[p] = cur_id;
+            world2image(cam, T, point_pos + 3 * p, px);  // reprojectPoint (:481-492)
+            if (!in_frame(cam, px, 3.0)) continue;
+            const uint32_t cell = (uint32_t)(int32_t)px[1] / (uint32_t)cell_size * (uint32_t)cols +
+                                  (uint32_t)(int32_t)px[0] / (uint32_t)cell_size;
+            cells[cell].push_back(f);
+            ++overlap[k];
+        }
+    }
+    int32_t m = 0, t = 0, ns = 0;
+    for (int32_t i = 0; i < n_cells; ++i) {  // (:463-477)
+        const int32_t idx = cell_order[i];
+        std::vector<int32_t>& c = cells[idx];
+        if (!c.empty()) {
+            // reprojectCell (:505-570): std::sort by point type, descending (the reference's own
+            // comparator, so cells past 16 candidates keep libstdc++'s order), first non-deleted wins;
+            // its FeatureAlignment result is not used to accept or reject
+            std::sort(c.begin(), c.end(), [&](int32_t a, int32_t b) { return point_type[feat_point[a]] > point_type[feat_point[b]]; });
+            for (int32_t f : c) {
+                ++t;
+                if (point_type[feat_point[f]] == 1u) continue;  // Point::PointType::DELETED
+                sel_feat[ns] = f;
+                sel_cell[ns] = idx;
+                world2image(cam, T, point_pos + 3 * feat_point[f], sel_px + 2 * ns);
+                ++ns;
+                ++m;
+                break;
+            }
+        }
+        if (m > 150) break;
+    }
+    *n_sel = ns;
+    *matches = m;
+    *trials = t;
     return SVO_OK;
 }
 

@@ -171,3 +171,84 @@ def make_shifted_plane(seed=7, width=320, height=120, fx=300.0, depth=10.0, disp
     d = depth / bearing[:, 2]  # distance along the bearing to the plane z = depth
     return DepthProblem(cam, kf_img, cur_img, np.array([0, 0, 0, 1, 0, 0, 0], np.float64), cur_pose, px, bearing, d,
                         float(np.median(d) * 1.03), float(depth_min))
+
+
+@dataclass
+class MapProblem:
+    """A map for Map::reprojectMap / addCandidateToFrame (SURVEY.md §8(f) row 1), from a config-2 scene:
+    the ref frame's and its last keyframe's features observe points; some lastKF features share a ref
+    feature's point (so the per-frame projection flag matters), point types are mixed (DELETED cells are
+    skipped), success counters sit around the promotion threshold, and lastKF features without a point
+    become depth-filter candidates for addCandidateToFrame."""
+    camera: dict
+    ref_img: np.ndarray
+    kf_img: np.ndarray
+    cur_img: np.ndarray
+    ref_pose: np.ndarray
+    kf_pose: np.ndarray
+    cur_pose: np.ndarray
+    n_ref: int
+    n_kf: int
+    feat_px: np.ndarray      # (n_ref + n_kf, 2): ref features, then lastKF features
+    feat_point: np.ndarray   # (n,) point index or -1
+    point_pos: np.ndarray    # (n_points, 3)
+    point_type: np.ndarray   # (n_points,) uint32 Point::PointType
+    point_succ: np.ndarray   # (n_points,) uint32 m_succeededProjection
+    cand_feat: np.ndarray    # (n_cand,) feature indices (lastKF features without a point)
+    cand_pos: np.ndarray     # (n_cand, 3) their converged points
+    cell_size: int = 30      # config "cell_pixel_size"
+
+
+def make_map_problem(seed=SEED_BASE, n_features=2000, share=0.2, cand_frac=0.15, nthreads=8):
+    s = make_pair(seed=seed, n_features=n_features, nthreads=nthreads, cell_order=30)
+    rng = np.random.default_rng(seed ^ 0x3A9)
+    n = s.n_ref + s.n_kf
+    feat_point = np.full(n, -1, np.int32)
+    pos = []
+    for f in range(n):
+        if s.has_point[f]:
+            feat_point[f] = len(pos)
+            pos.append(s.point[f])
+    pos = np.array(pos)
+    kf_idx = np.arange(s.n_ref, n)
+    cand = rng.choice(kf_idx, size=int(cand_frac * s.n_kf), replace=False)
+    cand.sort()
+    cand_pos = pos[feat_point[cand]].copy()
+    feat_point[cand] = -1
+    rest = np.setdiff1d(kf_idx, cand)
+    shared = rng.choice(rest, size=int(share * len(rest)), replace=False)
+    feat_point[shared] = rng.integers(0, s.n_ref, size=len(shared))  # ref features' points (index = ref feature)
+    npt = len(pos)
+    ptype = rng.choice(np.array([0, 1, 2, 3], np.uint32), size=npt, p=[0.2, 0.1, 0.2, 0.5]).astype(np.uint32)
+    psucc = rng.integers(0, 13, size=npt).astype(np.uint32)
+    return MapProblem(s.camera, s.ref_img, s.kf_img, s.cur_img, s.ref_pose, s.kf_pose, s.cur_true_pose, s.n_ref, s.n_kf,
+                      s.px.copy(), feat_point, pos, ptype, psucc, cand, cand_pos)
+
+
+def map_objects(p, levels=1, ctx=None, seed=0):
+    """The svo_amd object graph of a MapProblem: (map, ref frame, last keyframe, cur frame, points)."""
+    import svo_amd
+    c = p.camera
+    cam = svo_amd.PinholeCamera(c["width"], c["height"], c["fx"], c["fy"], c["cx"], c["cy"])
+    kf = svo_amd.Frame(cam, p.kf_img, levels, ctx=ctx)
+    kf.abs_pose[:] = p.kf_pose
+    ref = svo_amd.Frame(cam, p.ref_img, levels, last_keyframe=kf, ctx=ctx)
+    ref.abs_pose[:] = p.ref_pose
+    cur = svo_amd.Frame(cam, p.cur_img, levels, last_keyframe=kf, ctx=ctx)
+    cur.abs_pose[:] = p.cur_pose
+    points = []
+    for i in range(len(p.point_pos)):
+        pt = svo_amd.Point(p.point_pos[i])
+        pt.type = int(p.point_type[i])
+        pt.succeeded_projection = int(p.point_succ[i])
+        points.append(pt)
+    feats = []
+    for f in range(p.n_ref + p.n_kf):
+        fr = ref if f < p.n_ref else kf
+        ft = svo_amd.Feature(fr, p.feat_px[f], 0, point=points[p.feat_point[f]] if p.feat_point[f] >= 0 else None)
+        fr.add_feature(ft)
+        feats.append(ft)
+    m = svo_amd.Map(cam, p.cell_size, seed=seed, ctx=ctx)
+    for i, f in enumerate(p.cand_feat):
+        m.add_new_candidate(feats[f], svo_amd.Point(p.cand_pos[i]))
+    return m, ref, kf, cur, points, feats
