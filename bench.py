@@ -225,6 +225,44 @@ def secondary(args, ctx, scene, cam, camera, reps=20):
         "seeds": len(seeds), "gpu_ms_per_call": round(g * 1e3, 4), "seeds_per_s": round(len(seeds) / g, 1),
         "cpu_ms_1_thread": round(c * 1e3, 3), "outcomes": np.bincount(out[1], minlength=5).tolist(),
         "outcomes_match_oracle": bool(np.array_equal(out[1], oc[1]))}
+    # Map::reprojectMap + addCandidateToFrame on a config-2 map (ref frame + last
+    # keyframe, 2000 features, 150 depth-filter candidates): host plan + one batched FeatureAlignment
+    # launch per call, against the oracle's one-alignment-at-a-time restatement.  Fresh object graphs
+    # per repetition (the calls mutate the map), built outside the timed region.
+    mp = synth.make_map_problem()
+    graphs = [synth.map_objects(mp, ctx=ctx) for _ in range(reps + 1)]
+    news = []
+    t0 = None
+    for i, (m, ref, _, cur, _, _) in enumerate(graphs):
+        if i == 1:
+            t0 = time.perf_counter()
+        m.reproject_map(ref, cur, [])
+        m.add_candidate_to_frame(cur)
+        news.append(np.array([f.pixel_position for f in cur.features]))
+    g = (time.perf_counter() - t0) / reps
+    gr = {k: O.unpack_levels(O.build_pyramid(img, 1)[1], cam["width"], cam["height"], 1)[0]
+          for k, img in (("ref", mp.ref_img), ("kf", mp.kf_img), ("cur", mp.cur_img))}
+    m0 = graphs[0][0]
+    ptype, psucc = mp.point_type.copy(), mp.point_succ.copy()
+    plast = np.full(len(mp.point_pos), np.uint64(2 ** 64 - 1), np.uint64)
+    visited = np.zeros(len(m0.cell_orders), np.uint8)
+    t0 = time.perf_counter()
+    rep = O.reproject_map(mp.camera, mp.cell_size, m0.cell_orders, mp.cur_pose, graphs[0][3].id, gr["cur"],
+                          [gr["ref"], gr["kf"]], np.array([0, mp.n_ref, mp.n_ref + mp.n_kf], np.int32), mp.feat_px,
+                          mp.feat_point, mp.point_pos, ptype, psucc, plast, visited)
+    cm, cpx = O.add_candidates(mp.camera, mp.cell_size, visited, mp.cur_pose, gr["cur"], [gr["kf"]] * len(mp.cand_feat),
+                               mp.feat_px[mp.cand_feat], mp.cand_pos)
+    c = time.perf_counter() - t0
+    expect = np.concatenate([rep[1], cpx[cm]])
+    for _, ref, kf, cur, _, _ in graphs:  # release the device pyramids now (Frame <-> Feature cycles)
+        for fr in (ref, kf, cur):
+            fr.image_pyramid.clear()
+    del graphs
+    res["map_reproject"] = {
+        "map_points": len(mp.point_pos), "candidates": len(mp.cand_feat), "matches": int(rep[4]),
+        "new_features": int(len(expect)), "gpu_ms_per_call": round(g * 1e3, 4), "cpu_ms_1_thread": round(c * 1e3, 3),
+        "bitexact_vs_oracle": bool(np.array_equal(news[0], expect)),
+        "note": "end to end per frame, host bookkeeping included (Python mirror)"}
     return res
 
 

@@ -129,9 +129,11 @@ class PyramidSet:
         return out
 
     def close(self):
-        if getattr(self, "handle", None):
+        # only while the owning context lives: objects kept alive by reference cycles (Frame <-> Feature)
+        # may be finalized after their context at interpreter exit
+        if getattr(self, "handle", None) and getattr(self.ctx, "handle", None):
             lib().svo_pyramid_set_destroy(self.handle)
-            self.handle = None
+        self.handle = None
 
     def __del__(self):
         try:
@@ -332,9 +334,9 @@ class AlignBatch:
         return out
 
     def close(self):
-        if getattr(self, "handle", None):
+        if getattr(self, "handle", None) and getattr(self.ctx, "handle", None):
             lib().svo_align_batch_destroy(self.handle)
-            self.handle = None
+        self.handle = None
 
     def __del__(self):
         try:
