@@ -221,9 +221,14 @@ class Feature:
         self.frame = frame
         self.pixel_position = np.asarray(pixel_position, dtype=np.float64)
         self.level = level
-        self.bearing_vec = (np.asarray(bearing, np.float64) if bearing is not None
-                            else frame.camera.inverse_project2d(self.pixel_position))
+        self._bearing = None if bearing is None else np.asarray(bearing, np.float64)
         self.point = point
+
+    @property
+    def bearing_vec(self):  # formed on first use (the map creates many features that never need it)
+        if self._bearing is None:
+            self._bearing = self.frame.camera.inverse_project2d(self.pixel_position)
+        return self._bearing
 
     def set_point(self, point):
         self.point = point

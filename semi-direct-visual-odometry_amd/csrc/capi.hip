@@ -61,7 +61,26 @@ struct svo_ctx {
     hipStream_t sides[4];         // extra streams: a batch runs as concurrent sub-batch chains
     hipEvent_t fork, joins[4];    // sides wait for stream at fork; stream waits for each side at its join
     hipEvent_t events[16];
+    // grow-only scratch of the synchronous per-call entry points (FeatureAlignment): no device
+    // allocation per call once warm
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
 };
+
+// at least `bytes` of the context's scratch (the previous contents are not kept)
+static hipError_t ctx_scratch(svo_ctx* c, size_t bytes, void** out) {
+    if (bytes > c->scratch_bytes) {
+        if (c->scratch) (void)hipFree(c->scratch);
+        c->scratch = nullptr;
+        c->scratch_bytes = 0;
+        const size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes + bytes / 2;
+        const hipError_t e = hipMalloc(&c->scratch, want);
+        if (e != hipSuccess) return e;
+        c->scratch_bytes = want;
+    }
+    *out = c->scratch;
+    return hipSuccess;
+}
 
 struct svo_pyramid_set {
     svo_ctx* ctx;
@@ -147,6 +166,7 @@ int svo_ctx_destroy(svo_ctx* c) {
         if (c->joins[i]) (void)hipEventDestroy(c->joins[i]);
         if (c->sides[i]) (void)hipStreamDestroy(c->sides[i]);
     }
+    if (c->scratch) (void)hipFree(c->scratch);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SVO_OK;
@@ -517,15 +537,17 @@ static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_s
                               double* px_inout, double* err, int32_t* status) {
     SVO_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    const uint8_t** d_rg = nullptr;
-    int32_t* d_st = nullptr;
-    double *d_rpx = nullptr, *d_px = nullptr, *d_err = nullptr;
-    hipError_t e = hipMalloc(&d_rg, n * sizeof(void*));
-    if (e == hipSuccess) e = hipMalloc(&d_st, n * sizeof(int32_t));
-    if (e == hipSuccess) e = hipMalloc(&d_rpx, n * 2 * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&d_px, n * 2 * sizeof(double));
-    if (e == hipSuccess) e = hipMalloc(&d_err, n * sizeof(double));
-    if (e == hipSuccess) e = hipMemcpyAsync(d_rg, rg.data(), n * sizeof(void*), hipMemcpyHostToDevice, s);
+    // one scratch block: ref planes | ref px | px | err | status (8-B aligned pieces)
+    const size_t nn = (size_t)n;
+    void* base = nullptr;
+    hipError_t e = ctx_scratch(c, nn * (sizeof(void*) + 5 * sizeof(double) + 8), &base);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
+    const uint8_t** d_rg = static_cast<const uint8_t**>(base);
+    double* d_rpx = reinterpret_cast<double*>(d_rg + nn);
+    double* d_px = d_rpx + 2 * nn;
+    double* d_err = d_px + 2 * nn;
+    int32_t* d_st = reinterpret_cast<int32_t*>(d_err + nn);
+    e = hipMemcpyAsync(d_rg, rg.data(), n * sizeof(void*), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_rpx, ref_px, n * 2 * sizeof(double), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_px, px_inout, n * 2 * sizeof(double), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
@@ -548,8 +570,6 @@ static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_s
     if (e == hipSuccess && err) e = hipMemcpyAsync(err, d_err, n * sizeof(double), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && status) e = hipMemcpyAsync(status, d_st, n * sizeof(int32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    for (void* p : {(void*)d_rg, (void*)d_st, (void*)d_rpx, (void*)d_px, (void*)d_err})
-        if (p) (void)hipFree(p);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
     return SVO_OK;
 }
