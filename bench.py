@@ -263,6 +263,45 @@ def secondary(args, ctx, scene, cam, camera, reps=20):
         "new_features": int(len(expect)), "gpu_ms_per_call": round(g * 1e3, 4), "cpu_ms_1_thread": round(c * 1e3, 3),
         "bitexact_vs_oracle": bool(np.array_equal(news[0], expect)),
         "note": "end to end per frame, host bookkeeping included (Python mirror)"}
+    # FeatureSelection on a KITTI-shaped keyframe (threshold 50, 200 candidates,
+    # bucketing in 30-px cells: src/system.cpp:253, config/config.json).  gpu = the whole call (device
+    # detection + D2H of the keys + host std::sort / SSC); detect_call = svo_feature_detect alone (2 kernels +
+    # the keys' D2H; the kernel times are in the rocprof summary).
+    fr = svo_amd.Frame(camera, scene.ref_img, 1, ctx=ctx)
+    fsel = svo_amd.FeatureSelection(cam["width"], cam["height"], 30, ctx=ctx)
+    fsel.gradient_magnitude_with_ssc(fr, 50, 200, True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fr.features = []
+        fsel.gradient_magnitude_with_ssc(fr, 50, 200, True)
+    g = (time.perf_counter() - t0) / reps
+    got = np.array([f.pixel_position for f in fr.features])
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fsel.detect(fr, 50)
+    det_ms = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    opx, _, _, nk = O.feature_select_ssc(scene.ref_img, 50, 200, True, 30)
+    c = time.perf_counter() - t0
+    fr.features = []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fr.features = []
+        fsel.gradient_magnitude_by_value(fr, 50)
+    gv = (time.perf_counter() - t0) / reps
+    gotv = np.array([f.pixel_position for f in fr.features])
+    t0 = time.perf_counter()
+    vpx, _, _ = O.feature_select_by_value(scene.ref_img, 50, 30)
+    cv = time.perf_counter() - t0
+    fr.image_pyramid.clear()
+    res["feature_selection"] = {
+        "keypoints": int(nk), "features": int(len(opx)), "gpu_ms_per_call": round(g * 1e3, 4),
+        "detect_call_ms": round(det_ms, 4), "cpu_ms_1_thread": round(c * 1e3, 3),
+        "bitexact_vs_oracle": bool(np.array_equal(got, opx)),
+        "by_value_gpu_ms_per_call": round(gv * 1e3, 4), "by_value_cpu_ms_1_thread": round(cv * 1e3, 3),
+        "by_value_bitexact_vs_oracle": bool(np.array_equal(gotv, vpx)),
+        "note": "gradientMagnitudeWithSSC end to end per keyframe (device detect + host sort/SSC, "
+                "Python mirror); ByValue: one device launch per call"}
     return res
 
 

@@ -234,6 +234,35 @@ int svo_depth_update(svo_ctx* ctx, const svo_camera* cam, int32_t n_kf, const sv
                      int32_t* n_seeds_out, int32_t* outcome, double* cand_points, int32_t* cand_seed,
                      int32_t* n_cand);
 
+/* ---------------------------------------------------------------- FeatureSelection
+ * Replaces FeatureSelection (src/feature_selection.cpp:19-287; constructed src/system.cpp:28 with the
+ * image size and cell_pixel_size, called :81, :252-254, :428-430).  Its bool occupancy grid of
+ * (height / cell_size + 1) rows x (width / cell_size + 1) columns (:19-25) is caller-owned bytes here
+ * (`occupancy`, row-major, 1 = occupied): setExistingFeatures / setCellInGridOccupancy (:268-282) mark
+ * it, the bucketing branches clear it on return (resetGridOccupancy, :75, :141).  The gradient magnitude
+ * is the frame's level-0 gradient plane (computeImageGradient :250-266 is the same
+ * Simd::AbsGradientSaturatedSum as the pyramid's); the orientation is 0 everywhere (:261).  Output
+ * features are in Frame::addFeature order: pixel (x, y) and response = gradient magnitude. */
+int svo_feature_grid_size(int32_t width, int32_t height, int32_t cell_size, int32_t* rows, int32_t* cols);
+/* Device step of gradientMagnitudeWithSSC (:38-50): the level-0 gradient pixels of `frame` above
+ * `threshold` in row-major order, as keys (response << 24 | y * width + x; width * height <= 2^24).
+ * keys: capacity entries.  Synchronous. */
+int svo_feature_detect(svo_ctx* ctx, const svo_pyramid_set* set, int32_t frame, int32_t threshold, int32_t capacity,
+                       uint32_t* keys, int32_t* n_keys);
+/* gradientMagnitudeWithSSC(frame, detectionThreshold, numberCandidate, useBucketing) (:27-89): device
+ * detection, then std::sort by response (reference comparator) and SSC (:166-248, tolerance 0.1) on the
+ * host.  n_keypoints (may be NULL): keypoints above the threshold.  Synchronous. */
+int svo_feature_select_ssc(svo_ctx* ctx, const svo_pyramid_set* set, int32_t frame, int32_t threshold,
+                           int32_t number_candidate, int32_t use_bucketing, int32_t cell_size, uint8_t* occupancy,
+                           int32_t capacity, double* px_out, double* response_out, int32_t* n_out, int32_t* n_keypoints);
+/* gradientMagnitudeByValue(frame, detectionThreshold, useBucketing = true) (:91-143): per free cell the
+ * first maximum in row-major order, kept if above the threshold; cells in row-major order.  The
+ * reference's useBucketing = false branch reads the 8-bit magnitude as float (:150) and is rejected.
+ * Synchronous. */
+int svo_feature_select_by_value(svo_ctx* ctx, const svo_pyramid_set* set, int32_t frame, int32_t threshold,
+                                int32_t cell_size, uint8_t* occupancy, int32_t capacity, double* px_out,
+                                double* response_out, int32_t* n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -313,3 +313,54 @@ def add_candidates(cam, cell_size, cell_visited, cur_pose, cur_grad, cand_grads,
                                 _p(np.ascontiguousarray(cur_pose, np.float64)), _p(np.ascontiguousarray(cur_grad, np.uint8)),
                                 n, gp, _p(cpx), _p(cpp), _p(matched), _p(new_px))
     return matched[:n].astype(bool), new_px[:n]
+
+
+# ---------------------------------------------------------------- FeatureSelection (feature_selection_oracle.cpp)
+def grid_shape(w, h, cell):
+    return h // cell + 1, w // cell + 1
+
+
+def ssc(x, y, num_ret, cols, rows, tolerance=0.1):
+    """FeatureSelection::SSC on keypoints already in sorted order; returns the selected indices."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(y, np.float32)
+    out = np.zeros(max(len(x), 1), np.int32)
+    n = lib().oracle_ssc(_p(x), _p(y), ctypes.c_int32(len(x)), ctypes.c_int32(num_ret), ctypes.c_float(tolerance),
+                         ctypes.c_int32(cols), ctypes.c_int32(rows), _p(out))
+    return out[:n]
+
+
+def feature_select_ssc(img, threshold, num_candidates, use_bucketing, cell_size, occupancy=None):
+    """gradientMagnitudeWithSSC on a base image: (px (n, 2), response (n,), occupancy after, n_keypoints)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    occ = np.zeros(grid_shape(w, h, cell_size), np.uint8) if occupancy is None else np.array(occupancy, np.uint8)
+    cap = w * h
+    px = np.zeros((cap, 2))
+    resp = np.zeros(cap)
+    nk = ctypes.c_int32()
+    n = lib().oracle_feature_select_ssc(_p(img), w, h, threshold, num_candidates, int(bool(use_bucketing)), cell_size,
+                                        _p(occ), cap, _p(px), _p(resp), ctypes.byref(nk))
+    assert n >= 0
+    return px[:n], resp[:n], occ, nk.value
+
+
+def feature_select_by_value(img, threshold, cell_size, occupancy=None):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    occ = np.zeros(grid_shape(w, h, cell_size), np.uint8) if occupancy is None else np.array(occupancy, np.uint8)
+    cap = occ.size
+    px = np.zeros((cap, 2))
+    resp = np.zeros(cap)
+    n = lib().oracle_feature_select_by_value(_p(img), w, h, threshold, cell_size, _p(occ), cap, _p(px), _p(resp))
+    assert n >= 0
+    return px[:n], resp[:n], occ
+
+
+
+def sort_responses(resp):
+    """libstdc++ std::sort's keypoint order for u8 responses (reference comparator, :53-54)."""
+    resp = np.ascontiguousarray(resp, np.uint8)
+    perm = np.zeros(max(len(resp), 1), np.int32)
+    lib().oracle_sort_responses(_p(resp), len(resp), _p(perm))
+    return perm[:len(resp)]

@@ -86,6 +86,12 @@ _SIGNATURES = [
     ("svo_depth_update", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_int32, c_void_p, c_int32, c_void_p, P_i32, c_void_p, c_void_p,
                                    c_void_p, P_i32]),
+    ("svo_feature_grid_size", c_int32, [c_int32, c_int32, c_int32, P_i32, P_i32]),
+    ("svo_feature_detect", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, P_i32]),
+    ("svo_feature_select_ssc", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                                         c_int32, c_void_p, c_void_p, P_i32, P_i32]),
+    ("svo_feature_select_by_value", c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_int32,
+                                              c_void_p, c_void_p, P_i32]),
 ]
 
 EXPORTED = [s[0] for s in _SIGNATURES]

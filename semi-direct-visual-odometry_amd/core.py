@@ -217,10 +217,17 @@ class Point:
 class Feature:
     """Feature(frame, pixelPosition, level) — bearing from the frame's camera (src/feature.cpp:14)."""
 
-    def __init__(self, frame, pixel_position, level=0, point=None, bearing=None):
+    # Feature::FeatureType (include/feature.hpp:19-23)
+    EDGE, CORNER = 0, 1
+
+    def __init__(self, frame, pixel_position, level=0, point=None, bearing=None, gradient_magnitude=1.0,
+                 gradient_orientation=0.0, feature_type=EDGE):
         self.frame = frame
         self.pixel_position = np.asarray(pixel_position, dtype=np.float64)
         self.level = level
+        self.gradient_magnitude = gradient_magnitude      # m_gradientMagnitude (src/feature.cpp:15,34)
+        self.gradient_orientation = gradient_orientation  # m_gradientOrientation
+        self.type = feature_type
         self._bearing = None if bearing is None else np.asarray(bearing, np.float64)
         self.point = point
 
@@ -633,3 +640,82 @@ class DepthEstimator:
         self.features = [self.features[i] for i in keep]
         self.seeds = surv
         return new
+
+
+# ---------------------------------------------------------------- feature selection
+class FeatureSelection:
+    """FeatureSelection(width, height, cellSize) (src/feature_selection.cpp:19-287).
+
+    The occupancy grid ((height // cellSize + 1) x (width // cellSize + 1) cells) lives here on the host
+    like the reference's member; detection reads the frame's device-resident level-0 gradient plane."""
+
+    def __init__(self, width, height, cell_size, ctx=None):
+        self.ctx = ctx or default_context()
+        r, c = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().svo_feature_grid_size(int(width), int(height), int(cell_size), ctypes.byref(r), ctypes.byref(c)))
+        self.width, self.height, self.cell_size = int(width), int(height), int(cell_size)
+        self.grid_rows, self.grid_cols = r.value, c.value
+        self.occupancy_grid = np.zeros((self.grid_rows, self.grid_cols), np.uint8)
+        self.last_keypoints = 0
+
+    def set_existing_features(self, features):  # :268-274
+        for f in features:
+            self.set_cell_in_grid_occupancy(f.pixel_position)
+
+    def set_cell_in_grid_occupancy(self, location):  # :276-282 (uint32 truncation of the division)
+        self.occupancy_grid[int(location[1] / self.cell_size), int(location[0] / self.cell_size)] = 1
+
+    def reset_grid_occupancy(self):  # :284-287
+        self.occupancy_grid[:] = 0
+
+    def _emit(self, frame, px, resp, n):
+        for i in range(n):
+            frame.add_feature(Feature(frame, px[i].copy(), 0, gradient_magnitude=float(resp[i]),
+                                      gradient_orientation=0.0, feature_type=Feature.EDGE))
+        return n
+
+    def detect(self, frame, detection_threshold):
+        """The device step alone: keys (response << 24 | y * width + x) above the threshold, row-major."""
+        cap = self.width * self.height
+        keys = np.zeros(cap, np.uint32)
+        n = ctypes.c_int32()
+        check(lib().svo_feature_detect(self.ctx.handle, frame.image_pyramid.set.handle, 0, int(detection_threshold),
+                                       cap, ptr(keys), ctypes.byref(n)))
+        return keys[:n.value]
+
+    def gradient_magnitude_with_ssc(self, frame, detection_threshold, number_candidate, use_bucketing):
+        """:27-89 — adds the selected features to `frame` (EDGE, level 0); returns how many."""
+        cap = self.grid_rows * self.grid_cols if use_bucketing else max(4 * int(number_candidate), 1024)
+        while True:
+            px = np.zeros((cap, 2))
+            resp = np.zeros(cap)
+            n, nk = ctypes.c_int32(), ctypes.c_int32()
+            occ = self.occupancy_grid.copy()
+            rc = lib().svo_feature_select_ssc(self.ctx.handle, frame.image_pyramid.set.handle, 0,
+                                              int(detection_threshold), int(number_candidate), int(bool(use_bucketing)),
+                                              self.cell_size, ptr(occ), cap, ptr(px), ptr(resp), ctypes.byref(n),
+                                              ctypes.byref(nk))
+            if rc == _capi.SVO_ERR_ARG and not use_bucketing and cap < self.width * self.height:
+                cap = self.width * self.height  # SSC kept more than the first guess
+                continue
+            check(rc)
+            break
+        self.occupancy_grid[:] = occ
+        self.last_keypoints = nk.value
+        return self._emit(frame, px, resp, n.value)
+
+    def gradient_magnitude_by_value(self, frame, detection_threshold, use_bucketing=True):
+        """:91-143 — bucketing branch (the reference's other branch reads the 8-bit magnitude as float)."""
+        if not use_bucketing:
+            raise ValueError("gradientMagnitudeByValue without bucketing reads the u8 magnitude as float "
+                             "(src/feature_selection.cpp:150); not supported")
+        cap = self.grid_rows * self.grid_cols
+        px = np.zeros((cap, 2))
+        resp = np.zeros(cap)
+        n = ctypes.c_int32()
+        occ = self.occupancy_grid.copy()
+        check(lib().svo_feature_select_by_value(self.ctx.handle, frame.image_pyramid.set.handle, 0,
+                                                int(detection_threshold), self.cell_size, ptr(occ), cap, ptr(px),
+                                                ptr(resp), ctypes.byref(n)))
+        self.occupancy_grid[:] = occ
+        return self._emit(frame, px, resp, n.value)

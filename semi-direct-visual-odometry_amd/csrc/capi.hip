@@ -795,4 +795,135 @@ int svo_depth_update(svo_ctx* c, const svo_camera* cam, int32_t n_kf, const svo_
     return SVO_OK;
 }
 
+// ------------------------------------------------------------------ feature selection
+int svo_feature_grid_size(int32_t width, int32_t height, int32_t cell_size, int32_t* rows, int32_t* cols) {
+    if (!rows || !cols) return fail(SVO_ERR_ARG, "null argument");
+    if (width < 1 || height < 1 || cell_size < 1) return fail(SVO_ERR_ARG, "bad grid geometry");
+    *rows = height / cell_size + 1;  // src/feature_selection.cpp:21-22
+    *cols = width / cell_size + 1;
+    return SVO_OK;
+}
+
+static int fs_check(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t threshold) {
+    if (!c || !p) return fail(SVO_ERR_ARG, "null argument");
+    if (p->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
+    if (frame < 0 || frame >= p->n_frames) return fail(SVO_ERR_ARG, "frame %d out of range", frame);
+    if (threshold < 0) return fail(SVO_ERR_ARG, "threshold < 0");
+    if ((int64_t)p->width * p->height >= ((int64_t)1 << 24)) return fail(SVO_ERR_ARG, "image of 2^24 pixels or more");
+    return SVO_OK;
+}
+
+// device detection into host keys; *n = keys above the threshold (may exceed capacity: nothing copied then)
+static int fs_detect(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t threshold, int32_t capacity,
+                     uint32_t* keys, int32_t* n) {
+    SVO_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int64_t npx = (int64_t)p->width * p->height;
+    const int nseg = svo::feature_detect_segments(npx);
+    void* base = nullptr;
+    hipError_t e = ctx_scratch(c, (size_t)npx * 4 + (size_t)nseg * 4 + 64, &base);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_detect: %s", hipGetErrorString(e));
+    uint32_t* d_keys = static_cast<uint32_t*>(base);
+    int* d_n = reinterpret_cast<int*>(d_keys + npx);
+    int* d_seg = d_n + 16;
+    const uint8_t* plane = p->d_base + (size_t)frame * p->stride + p->grad_off;
+    svo::launch_feature_detect(plane, p->width, p->height, threshold, d_seg, d_keys, d_n, s);
+    e = hipGetLastError();
+    int32_t cnt = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&cnt, d_n, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && cnt <= capacity && cnt > 0) e = hipMemcpy(keys, d_keys, (size_t)cnt * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_detect: %s", hipGetErrorString(e));
+    *n = cnt;
+    return SVO_OK;
+}
+
+int svo_feature_detect(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t threshold, int32_t capacity,
+                       uint32_t* keys, int32_t* n_keys) {
+    if (int r = fs_check(c, p, frame, threshold)) return r;
+    if (!n_keys || (capacity > 0 && !keys)) return fail(SVO_ERR_ARG, "null argument");
+    if (int r = fs_detect(c, p, frame, threshold, capacity, keys, n_keys)) return r;
+    if (*n_keys > capacity) return fail(SVO_ERR_ARG, "%d keypoints exceed capacity %d", *n_keys, capacity);
+    return SVO_OK;
+}
+
+int svo_feature_select_ssc(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t threshold,
+                           int32_t number_candidate, int32_t use_bucketing, int32_t cell_size, uint8_t* occupancy,
+                           int32_t capacity, double* px_out, double* response_out, int32_t* n_out, int32_t* n_keypoints) {
+    if (int r = fs_check(c, p, frame, threshold)) return r;
+    if (!n_out || (capacity > 0 && (!px_out || !response_out))) return fail(SVO_ERR_ARG, "null argument");
+    if (number_candidate < 2) return fail(SVO_ERR_ARG, "numberCandidate < 2 (SSC divides by numberCandidate - 1)");
+    if (use_bucketing && (cell_size < 1 || !occupancy)) return fail(SVO_ERR_ARG, "bucketing needs cell_size and occupancy");
+    const int32_t W = p->width, H = p->height;
+    std::vector<uint32_t> keys((size_t)W * H);
+    int32_t n = 0;
+    if (int r = fs_detect(c, p, frame, threshold, (int32_t)keys.size(), keys.data(), &n)) return r;
+    if (n_keypoints) *n_keypoints = n;
+    svo::feature_sort_keys(keys.data(), n);  // :53-54
+    std::vector<int32_t> xs(n), ys(n), sel;
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t idx = (int32_t)(keys[i] & 0xFFFFFFu);
+        ys[i] = idx / W;
+        xs[i] = idx - ys[i] * W;
+    }
+    svo::feature_ssc(xs.data(), ys.data(), n, number_candidate, 0.1f, W, H, sel);  // :57-58
+    const int32_t gcols = use_bucketing ? W / cell_size + 1 : 0;
+    int32_t m = 0;
+    for (int32_t i : sel) {
+        if (use_bucketing) {  // :60-76
+            uint8_t& cell = occupancy[(xs[i] / cell_size) + (ys[i] / cell_size) * gcols];
+            if (cell) continue;
+            cell = 1;
+        }
+        if (m >= capacity) return fail(SVO_ERR_ARG, "more than capacity %d features", capacity);
+        px_out[2 * m] = xs[i];
+        px_out[2 * m + 1] = ys[i];
+        response_out[m] = (double)(keys[i] >> 24);
+        ++m;
+    }
+    if (use_bucketing) std::memset(occupancy, 0, (size_t)(H / cell_size + 1) * gcols);  // resetGridOccupancy
+    *n_out = m;
+    return SVO_OK;
+}
+
+int svo_feature_select_by_value(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t threshold,
+                                int32_t cell_size, uint8_t* occupancy, int32_t capacity, double* px_out,
+                                double* response_out, int32_t* n_out) {
+    if (int r = fs_check(c, p, frame, threshold)) return r;
+    if (!occupancy || !n_out || (capacity > 0 && (!px_out || !response_out))) return fail(SVO_ERR_ARG, "null argument");
+    if (cell_size < 1 || cell_size > 1024) return fail(SVO_ERR_ARG, "cell_size must be in [1, 1024]");
+    const int32_t W = p->width, H = p->height, gr = H / cell_size + 1, gc = W / cell_size + 1, nc = gr * gc;
+    SVO_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    void* base = nullptr;
+    hipError_t e = ctx_scratch(c, (size_t)nc * 5 + 64, &base);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_select_by_value: %s", hipGetErrorString(e));
+    uint32_t* d_px = static_cast<uint32_t*>(base);
+    uint8_t* d_occ = reinterpret_cast<uint8_t*>(d_px + nc);
+    std::vector<uint32_t> cell_px(nc);
+    e = hipMemcpyAsync(d_occ, occupancy, nc, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        const uint8_t* plane = p->d_base + (size_t)frame * p->stride + p->grad_off;
+        svo::launch_feature_cell_max(plane, W, H, cell_size, gr, gc, d_occ, threshold, d_px, s);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(cell_px.data(), d_px, (size_t)nc * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_select_by_value: %s", hipGetErrorString(e));
+    int32_t m = 0;
+    for (int32_t k = 0; k < nc; ++k) {
+        const uint32_t v = (uint32_t)cell_px[k];
+        if (v == 0xFFFFFFFFu) continue;
+        if (m >= capacity) return fail(SVO_ERR_ARG, "more than capacity %d features", capacity);
+        const int32_t idx = (int32_t)(v & 0xFFFFFFu);
+        px_out[2 * m] = idx % W;
+        px_out[2 * m + 1] = idx / W;
+        response_out[m] = (double)(v >> 24);
+        ++m;
+    }
+    std::memset(occupancy, 0, nc);  // resetGridOccupancy (:141)
+    *n_out = m;
+    return SVO_OK;
+}
+
 }  // extern "C"

@@ -105,4 +105,17 @@ struct DepthArgs {
 };
 void launch_depth_update(const DepthArgs& a, hipStream_t s);
 
+// FeatureSelection (feature_select.hip)
+int feature_detect_segments(int64_t npx);
+void launch_feature_detect(const uint8_t* plane, int width, int height, int thr, int* seg_counts, uint32_t* keys,
+                           int* n_keys, hipStream_t s);
+void launch_feature_cell_max(const uint8_t* plane, int width, int height, int cell, int grid_rows, int grid_cols,
+                             const uint8_t* occupancy, int thr, uint32_t* cell_px, hipStream_t s);
+}  // namespace svo
+
+#include <vector>
+namespace svo {
+void feature_sort_keys(uint32_t* keys, int32_t n);
+void feature_ssc(const int32_t* xs, const int32_t* ys, int32_t n, int32_t num_ret, float tolerance, int32_t cols,
+                 int32_t rows, std::vector<int32_t>& out);
 }  // namespace svo
