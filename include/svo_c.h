@@ -263,6 +263,16 @@ int svo_feature_select_by_value(svo_ctx* ctx, const svo_pyramid_set* set, int32_
                                 int32_t cell_size, uint8_t* occupancy, int32_t capacity, double* px_out,
                                 double* response_out, int32_t* n_out);
 
+/* ---------------------------------------------------------------- trajectory output (host only)
+ * System::writeInFile (src/system.cpp:635-640, called per image from src/main.cpp:114-121): the ref
+ * frame's camera->world pose m_absPose.inverse().matrix3x4() (Sophus) as one KITTI trajectory line.
+ * out12: that 3x4 matrix, row-major. */
+int svo_pose_matrix3x4_inverse(const double* pose, double* out12);
+/* The same line as text: the 12 numbers row-major, single spaces, each as an std::ostream with
+ * precision 6 prints a double ("%.6g"; Eigen IOFormat utils::eigenFormatIO, src/utils.cpp:10-13), NUL
+ * terminated, no newline.  cap: bytes of buf (>= 12 * 14 is always enough). */
+int svo_format_kitti_pose(const double* pose, char* buf, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

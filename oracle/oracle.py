@@ -364,3 +364,22 @@ def sort_responses(resp):
     perm = np.zeros(max(len(resp), 1), np.int32)
     lib().oracle_sort_responses(_p(resp), len(resp), _p(perm))
     return perm[:len(resp)]
+
+
+# ---------------------------------------------------------------- trajectory / feature dump text
+def kitti_line(pose):
+    """System::writeInFile's line for a world->camera pose (Sophus params)."""
+    pose = np.ascontiguousarray(pose, np.float64)
+    buf = ctypes.create_string_buffer(512)
+    n = lib().oracle_kitti_line(_p(pose), buf, 512)
+    assert n >= 0
+    return buf.value.decode()
+
+
+def stream_g6(v):
+    """`std::ostream << std::setprecision(6) << v` for one double."""
+    buf = ctypes.create_string_buffer(64)
+    lib().oracle_stream_g6.argtypes = [ctypes.c_double, ctypes.c_char_p, ctypes.c_int32]
+    n = lib().oracle_stream_g6(float(v), buf, 64)
+    assert n >= 0
+    return buf.value.decode()

@@ -33,6 +33,9 @@
 #include <cstdint>
 #include <cstring>
 #include <functional>
+#include <iomanip>
+#include <sstream>
+#include <string>
 #include <limits>
 #include <thread>
 #include <vector>
@@ -1167,6 +1170,41 @@ void oracle_add_candidates(const oc_camera* c, int32_t cell_size, uint8_t* cell_
             cell_visited[k] = 1;
         }
     }
+}
+
+// System::writeInFile (src/system.cpp:635-640): m_absPose.inverse().matrix3x4() streamed with
+// std::setprecision(6) through Eigen's IOFormat(6, DontAlignCols, " ", " ", "", "", "", "")
+// (src/utils.cpp:10-13): coefficients of a row joined by the coefficient separator, rows by the row
+// separator, no prefixes.  Returns the line length (without newline), -1 if cap is short.
+int32_t oracle_kitti_line(const double* pose, char* buf, int32_t cap) {
+    const SE3 T{{pose[0], pose[1], pose[2], pose[3]}, {pose[4], pose[5], pose[6]}};
+    const SE3 Ti = inverse(T);
+    double R[3][3];
+    rotmat(Ti.q, R);
+    const double t[3] = {Ti.t.x, Ti.t.y, Ti.t.z};
+    std::ostringstream os;
+    os << std::setprecision(6);
+    for (int r = 0; r < 3; ++r) {
+        if (r) os << " ";                         // rowSeparator
+        for (int c = 0; c < 4; ++c) {
+            if (c) os << " ";                     // coeffSeparator
+            os << (c < 3 ? R[r][c] : t[r]);
+        }
+    }
+    const std::string line = os.str();
+    if ((int32_t)line.size() + 1 > cap) return -1;
+    std::memcpy(buf, line.c_str(), line.size() + 1);
+    return (int32_t)line.size();
+}
+
+// one double as `stream << std::setprecision(6) << v` (utils::writeAllInfoFile, src/utils.cpp:62-70)
+int32_t oracle_stream_g6(double v, char* buf, int32_t cap) {
+    std::ostringstream os;
+    os << std::setprecision(6) << v;
+    const std::string s = os.str();
+    if ((int32_t)s.size() + 1 > cap) return -1;
+    std::memcpy(buf, s.c_str(), s.size() + 1);
+    return (int32_t)s.size();
 }
 
 }  // extern "C"

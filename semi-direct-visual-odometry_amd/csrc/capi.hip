@@ -926,4 +926,35 @@ int svo_feature_select_by_value(svo_ctx* c, const svo_pyramid_set* p, int32_t fr
     return SVO_OK;
 }
 
+// ------------------------------------------------------------------ trajectory output
+int svo_pose_matrix3x4_inverse(const double* pose, double* out12) {
+    if (!pose || !out12) return fail(SVO_ERR_ARG, "null argument");
+    const svo::SE3 T{{pose[0], pose[1], pose[2], pose[3]}, {pose[4], pose[5], pose[6]}};
+    const svo::SE3 Ti = svo::se3_inverse(T);  // Sophus SE3::inverse
+    double R[3][3];
+    svo::rotmat(Ti.q, R);  // SO3::matrix (Eigen toRotationMatrix)
+    const double t[3] = {Ti.t.x, Ti.t.y, Ti.t.z};
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) out12[4 * r + c] = R[r][c];
+        out12[4 * r + 3] = t[r];
+    }
+    return SVO_OK;
+}
+
+int svo_format_kitti_pose(const double* pose, char* buf, int32_t cap) {
+    if (!buf || cap < 1) return fail(SVO_ERR_ARG, "null argument");
+    double m[12];
+    if (int r = svo_pose_matrix3x4_inverse(pose, m)) return r;
+    int32_t o = 0;
+    for (int i = 0; i < 12; ++i) {
+        const int k = std::snprintf(buf + o, (size_t)(cap - o), i ? " %.6g" : "%.6g", m[i]);
+        if (k < 0 || k >= cap - o) {
+            buf[0] = 0;
+            return fail(SVO_ERR_ARG, "buffer of %d bytes too short", cap);
+        }
+        o += k;
+    }
+    return SVO_OK;
+}
+
 }  // extern "C"

@@ -1,7 +1,9 @@
 // svo.cpp — implementation of the C++ class-surface mirror (host/svo.hpp) over the C ABI.
 #include "svo.hpp"
 
+#include <algorithm>
 #include <cmath>
+#include <iomanip>
 #include <string>
 
 namespace svo_amd {
@@ -122,5 +124,84 @@ double FeatureAlignment::align(const std::shared_ptr<Feature>& refFeature, const
                             pixelPos.data(), &err, &m_status));
     return err;
 }
+
+// ------------------------------------------------------------------ FeatureSelection
+FeatureSelection::FeatureSelection(Context& ctx, int32_t width, int32_t height, int32_t cellSize)
+    : m_ctx(ctx), m_width(width), m_height(height), m_cellSize(cellSize) {
+    check(svo_feature_grid_size(width, height, cellSize, &m_gridRows, &m_gridCols));
+    m_occupancyGrid.assign((size_t)m_gridRows * m_gridCols, 0);
+}
+
+void FeatureSelection::emit(std::shared_ptr<Frame>& frame, const std::vector<double>& px, const std::vector<double>& resp,
+                            int32_t n) {
+    for (int32_t i = 0; i < n; ++i) {  // Feature(frame, px, response, angle 0, level 0, EDGE) (:68-71)
+        auto f = std::make_shared<Feature>(frame.get(), Vec2{px[2 * i], px[2 * i + 1]});
+        f->m_gradientMagnitude = resp[i];
+        frame->m_features.push_back(std::move(f));
+    }
+}
+
+void FeatureSelection::gradientMagnitudeWithSSC(std::shared_ptr<Frame>& frame, uint32_t detectionThreshold,
+                                                uint32_t numberCandidate, bool useBucketing) {
+    const int32_t cap = useBucketing ? m_gridRows * m_gridCols : m_width * m_height;
+    std::vector<double> px(2 * (size_t)cap), resp(cap);
+    int32_t n = 0;
+    check(svo_feature_select_ssc(m_ctx.get(), frame->m_imagePyramid.set(), 0, (int32_t)detectionThreshold,
+                                 (int32_t)numberCandidate, useBucketing ? 1 : 0, m_cellSize, m_occupancyGrid.data(), cap,
+                                 px.data(), resp.data(), &n, nullptr));
+    emit(frame, px, resp, n);
+}
+
+void FeatureSelection::gradientMagnitudeByValue(std::shared_ptr<Frame>& frame, uint32_t detectionThreshold,
+                                                bool useBucketing) {
+    if (!useBucketing) throw Error(SVO_ERR_ARG, "svo: gradientMagnitudeByValue without bucketing is not supported");
+    const int32_t cap = m_gridRows * m_gridCols;
+    std::vector<double> px(2 * (size_t)cap), resp(cap);
+    int32_t n = 0;
+    check(svo_feature_select_by_value(m_ctx.get(), frame->m_imagePyramid.set(), 0, (int32_t)detectionThreshold,
+                                      m_cellSize, m_occupancyGrid.data(), cap, px.data(), resp.data(), &n));
+    emit(frame, px, resp, n);
+}
+
+void FeatureSelection::setExistingFeatures(const std::vector<std::shared_ptr<Feature>>& features) {
+    for (const auto& f : features) setCellInGridOccupancy(f->m_pixelPosition);
+}
+
+void FeatureSelection::setCellInGridOccupancy(const Vec2& location) {  // :276-282
+    const uint32_t idx = location[0] / m_cellSize;
+    const uint32_t idy = location[1] / m_cellSize;
+    m_occupancyGrid[idy * m_gridCols + idx] = 1;
+}
+
+void FeatureSelection::resetGridOccupancy() { std::fill(m_occupancyGrid.begin(), m_occupancyGrid.end(), 0); }
+
+// ------------------------------------------------------------------ trajectory / feature dump
+namespace utils {
+void writeInFile(const Pose& refAbsPose, std::ostream& w) {
+    double m[12];
+    check(svo_pose_matrix3x4_inverse(refAbsPose.data(), m));
+    w << std::setprecision(6);
+    for (int i = 0; i < 12; ++i) w << (i ? " " : "") << m[i];
+    w << std::endl;
+}
+
+void writeAllInfoFile(const Frame& ref, const Frame& cur, std::ostream& w) {
+    for (std::size_t i = 0; i < ref.numberObservation(); i++) {
+        const Vec2& r = ref.m_features[i]->m_pixelPosition;
+        const Vec2& c = cur.m_features[i]->m_pixelPosition;
+        const Vec3& p = ref.m_features[i]->m_point->m_position;
+        w << std::setprecision(6) << r[0] << " " << r[1] << " " << c[0] << " " << c[1] << " " << p[0] << " " << p[1]
+          << " " << p[2] << std::endl;
+    }
+}
+
+void writeFeaturesInfoFile(const Frame& ref, const Frame& cur, std::ostream& w) {
+    for (std::size_t i = 0; i < ref.numberObservation(); i++) {
+        const Vec2& r = ref.m_features[i]->m_pixelPosition;
+        const Vec2& c = cur.m_features[i]->m_pixelPosition;
+        w << std::setprecision(6) << r[0] << " " << r[1] << " " << c[0] << " " << c[1] << std::endl;
+    }
+}
+}  // namespace utils
 
 }  // namespace svo_amd

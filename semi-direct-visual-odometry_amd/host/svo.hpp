@@ -11,6 +11,7 @@
 #include <array>
 #include <cstdint>
 #include <memory>
+#include <ostream>
 #include <stdexcept>
 #include <vector>
 
@@ -79,10 +80,14 @@ struct Point {
     Vec3 m_position;
 };
 struct Feature {  // include/feature.hpp:14
+    enum class FeatureType : uint32_t { EDGE = 0, CORNER = 1 };  // include/feature.hpp:19-23
     Frame* m_frame;
     Vec2 m_pixelPosition;
     Vec3 m_bearingVec;
     std::shared_ptr<Point> m_point;
+    double m_gradientMagnitude = 1.0;    // src/feature.cpp:15
+    double m_gradientOrientation = 0.0;
+    FeatureType m_type = FeatureType::EDGE;
     Feature(Frame* frame, const Vec2& px);
 };
 struct Frame {  // include/frame.hpp:70-208 (the members the alignment path reads)
@@ -121,5 +126,36 @@ private:
     uint32_t m_patchSize;
     int32_t m_status = SVO_STATUS_FAILED;
 };
+
+// FeatureSelection (include/feature_selection.hpp, src/feature_selection.cpp:19-287): the occupancy grid
+// is a host member as in the reference; detection runs on the frame's device-resident gradient plane.
+class FeatureSelection {
+public:
+    FeatureSelection(Context& ctx, int32_t width, int32_t height, int32_t cellSize);
+    FeatureSelection(const FeatureSelection&) = delete;
+    FeatureSelection& operator=(const FeatureSelection&) = delete;
+    void gradientMagnitudeWithSSC(std::shared_ptr<Frame>& frame, uint32_t detectionThreshold, uint32_t numberCandidate,
+                                  bool useBucketing);
+    void gradientMagnitudeByValue(std::shared_ptr<Frame>& frame, uint32_t detectionThreshold, bool useBucketing);
+    void setExistingFeatures(const std::vector<std::shared_ptr<Feature>>& features);
+    void setCellInGridOccupancy(const Vec2& location);
+    void resetGridOccupancy();
+    const std::vector<uint8_t>& occupancyGrid() const { return m_occupancyGrid; }
+
+private:
+    void emit(std::shared_ptr<Frame>& frame, const std::vector<double>& px, const std::vector<double>& resp, int32_t n);
+    Context& m_ctx;
+    int32_t m_width, m_height, m_cellSize, m_gridRows, m_gridCols;
+    std::vector<uint8_t> m_occupancyGrid;
+};
+
+// Trajectory and feature-dump text, through std::ostream like the reference.
+namespace utils {
+// System::writeInFile (src/system.cpp:635-640): refAbsPose.inverse().matrix3x4() at precision 6
+void writeInFile(const Pose& refAbsPose, std::ostream& fileWriter);
+// utils::writeAllInfoFile / writeFeaturesInfoFile (src/utils.cpp:62-81)
+void writeAllInfoFile(const Frame& refFrame, const Frame& curFrame, std::ostream& fileWriter);
+void writeFeaturesInfoFile(const Frame& refFrame, const Frame& curFrame, std::ostream& fileWriter);
+}  // namespace utils
 
 }  // namespace svo_amd

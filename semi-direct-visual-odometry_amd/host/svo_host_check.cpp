@@ -1,0 +1,62 @@
+// svo_host_check.cpp — drives the C++ class-surface mirror (host/svo.hpp, libsvo_host.so) from the tests.
+//   svo_host_check io              poses on stdin (7 numbers a line, Sophus params) -> utils::writeInFile lines
+//   svo_host_check fs W H CELL THR NUM BUCKET IMAGE.raw [EX EY]...
+//                                  FeatureSelection::gradientMagnitudeWithSSC on a raw 8-bit image (GPU);
+//                                  existing features (EX, EY) marked first; prints "x y response" per feature
+//   svo_host_check fv W H CELL THR IMAGE.raw    gradientMagnitudeByValue (bucketing)
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <iterator>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "svo.hpp"
+
+using namespace svo_amd;
+
+static std::vector<uint8_t> read_raw(const char* path, size_t n) {
+    std::ifstream f(path, std::ios::binary);
+    std::vector<uint8_t> v((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (v.size() != n) throw std::runtime_error("image size mismatch");
+    return v;
+}
+
+int main(int argc, char** argv) {
+    try {
+        const std::string mode = argc > 1 ? argv[1] : "";
+        if (mode == "io") {
+            Pose p;
+            while (std::cin >> p[0] >> p[1] >> p[2] >> p[3] >> p[4] >> p[5] >> p[6]) utils::writeInFile(p, std::cout);
+            return 0;
+        }
+        if ((mode == "fs" && argc >= 9) || (mode == "fv" && argc >= 7)) {
+            const int w = std::atoi(argv[2]), h = std::atoi(argv[3]), cell = std::atoi(argv[4]), thr = std::atoi(argv[5]);
+            const char* img_path = mode == "fs" ? argv[8] : argv[6];
+            const std::vector<uint8_t> img = read_raw(img_path, (size_t)w * h);
+            Context ctx(0);
+            auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, 300.0, 300.0, w / 2.0, h / 2.0});
+            auto frame = std::make_shared<Frame>(ctx, cam, img.data(), 1);
+            FeatureSelection sel(ctx, w, h, cell);
+            if (mode == "fs") {
+                std::vector<std::shared_ptr<Feature>> existing;
+                for (int i = 9; i + 1 < argc; i += 2)
+                    existing.push_back(std::make_shared<Feature>(frame.get(), Vec2{std::atof(argv[i]), std::atof(argv[i + 1])}));
+                sel.setExistingFeatures(existing);
+                sel.gradientMagnitudeWithSSC(frame, thr, std::atoi(argv[6]), std::atoi(argv[7]) != 0);
+            } else {
+                sel.gradientMagnitudeByValue(frame, thr, true);
+            }
+            for (const auto& f : frame->m_features)
+                std::printf("%.17g %.17g %.17g\n", f->m_pixelPosition[0], f->m_pixelPosition[1], f->m_gradientMagnitude);
+            return 0;
+        }
+        std::fprintf(stderr, "usage: svo_host_check io | fs W H CELL THR NUM BUCKET IMAGE [EX EY]... | fv W H CELL THR IMAGE\n");
+        return 2;
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "svo_host_check: %s\n", e.what());
+        return 1;
+    }
+}
