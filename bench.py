@@ -302,6 +302,39 @@ def secondary(args, ctx, scene, cam, camera, reps=20):
         "by_value_bitexact_vs_oracle": bool(np.array_equal(gotv, vpx)),
         "note": "gradientMagnitudeWithSSC end to end per keyframe (device detect + host sort/SSC, "
                 "Python mirror); ByValue: one device launch per call"}
+    # BundleAdjustment::optimizePose for 512 frames of 1000 features each (85 % with a
+    # point, the flags a previous call left), one workgroup per frame, against the oracle on 32 of them.
+    rng = np.random.default_rng(4)
+    F, nfe = 512, 1000
+    P = rng.normal(size=(F * nfe, 3)) * [4, 2, 3] + [0, 0, 12]
+    bear = P / np.linalg.norm(P, axis=1, keepdims=True) + rng.normal(size=P.shape) * 2e-3
+    has = (rng.random(F * nfe) > 0.15).astype(np.uint8)
+    off = np.arange(F + 1, dtype=np.int32) * nfe
+    poses0 = np.tile(np.array([0, 0, 0, 1, 0.02, -0.01, 0.03]), (F, 1))
+    vis = has.copy()
+    pz = poses0.copy()
+    svo_amd.pose_optimize_batch(off, bear, P, has, vis, pz, ctx)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        vis[:] = has
+        pz[:] = poses0
+        err_b, st_b = svo_amd.pose_optimize_batch(off, bear, P, has, vis, pz, ctx)
+    g = (time.perf_counter() - t0) / reps
+    ns = 32
+    t0 = time.perf_counter()
+    worst = 0.0
+    for f in range(ns):
+        sl = slice(f * nfe, (f + 1) * nfe)
+        po, eo, so, _ = O.optimize_pose(bear[sl], P[sl], has[sl], has[sl], poses0[f])
+        q = pz[f] if np.dot(pz[f][:4], po[:4]) >= 0 else np.concatenate([-pz[f][:4], pz[f][4:]])
+        worst = max(worst, float(np.abs(q - po).max()))
+    c = (time.perf_counter() - t0) / ns
+    res["pose_ba"] = {
+        "frames": F, "features_per_frame": nfe, "gpu_ms_per_call": round(g * 1e3, 4),
+        "frames_per_s": round(F / g, 1), "cpu_ms_per_frame_1_thread": round(c * 1e3, 4),
+        "cpu_frames_per_s_1_thread": round(1.0 / c, 1), "max_abs_pose_diff_vs_oracle": worst,
+        "status_counts": np.bincount(st_b + 1, minlength=11).tolist(),
+        "note": "BundleAdjustment::optimizePose batched (H2D of the features included); oracle: 32 frames"}
     return res
 
 

@@ -273,6 +273,23 @@ int svo_pose_matrix3x4_inverse(const double* pose, double* out12);
  * terminated, no newline.  cap: bytes of buf (>= 12 * 14 is always enough). */
 int svo_format_kitti_pose(const double* pose, char* buf, int32_t cap);
 
+/* ---------------------------------------------------------------- pose-only bundle adjustment
+ * Replaces BundleAdjustment::optimizePose(frame) (src/bundle_adjustment.cpp:35-69; BundleAdjustment(camera,
+ * 0, 6) constructed src/system.cpp:31, the call itself is commented out at :388) for n_frames independent
+ * frames: one LM step of Optimizer::optimizeLM<SE3d> on |bearing - normalise(T * P)| (three rows per
+ * feature, only the third visible), pose <- exp(dx) * pose.  Frame f owns features feat_off[f] ..
+ * feat_off[f+1]-1: bearing (x3), point (x3, the feature's m_point->m_position), has_point (m_point != null).
+ * vis_inout is m_refVisibility of the BundleAdjustment object that optimises the frame, resized to the
+ * frame's feature count (new entries 0): the residual step reads the flags the PREVIOUS call left (the
+ * reference calls the residual functor before the Jacobian functor, src/optimizer.cpp:199 vs :242), so a
+ * fresh object returns NaN and leaves the pose as exp(0) * pose; on return the flags are has_point.
+ * poses_inout n_frames x 7; err: the returned RMSE (0 when the frame has no features, -1 on
+ * Non_Suff_Points); status: Optimizer::Status, -1 when nothing ran (no features).  A stale flag on a
+ * feature without a point (the reference dereferences null) is SVO_ERR_ARG.  Synchronous. */
+int svo_pose_optimize(svo_ctx* ctx, int32_t n_frames, const int32_t* feat_off, const double* bearing,
+                      const double* point, const uint8_t* has_point, uint8_t* vis_inout, double* poses_inout,
+                      double* err, int32_t* status);
+
 #ifdef __cplusplus
 }
 #endif

@@ -383,3 +383,23 @@ def stream_g6(v):
     n = lib().oracle_stream_g6(float(v), buf, 64)
     assert n >= 0
     return buf.value.decode()
+
+
+# ---------------------------------------------------------------- pose-only bundle adjustment
+def optimize_pose(bearing, point, has_point, vis_in, pose, median_mode=1):
+    """BundleAdjustment::optimizePose on one frame: (pose, err, status, vis_out); vis_in is the object's
+    m_refVisibility before the call (any length: resized like the member)."""
+    n = len(has_point)
+    bearing = np.ascontiguousarray(bearing, np.float64).reshape(-1, 3)
+    point = np.ascontiguousarray(point, np.float64).reshape(-1, 3)
+    has_point = np.ascontiguousarray(has_point, np.uint8)
+    vis = np.zeros(max(n, len(vis_in), 1), np.uint8)
+    vis[:len(vis_in)] = vis_in
+    pose = np.ascontiguousarray(pose, np.float64).copy()
+    err = ctypes.c_double()
+    st = ctypes.c_int32()
+    rc = lib().oracle_optimize_pose(n, _p(bearing), _p(point), _p(has_point), len(vis_in), _p(vis), _p(pose),
+                                    median_mode, ctypes.byref(err), ctypes.byref(st))
+    if rc != 0:
+        raise ValueError("stale visible flag on a feature without a point")
+    return pose, err.value, st.value, (vis[:n].copy() if n else np.array(vis_in, np.uint8))

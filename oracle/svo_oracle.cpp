@@ -404,7 +404,8 @@ struct Optimizer {
     // 0 (:186, :327 commented out) it always leaves after the first damped step (:328).
     template <typename T>
     std::pair<int32_t, double> optimize_lm(T& params, const std::function<uint32_t(T&)>& residual_fn,
-                                           const std::function<void(T&, const double*)>& update_fn) {
+                                           const std::function<void(T&, const double*)>& update_fn,
+                                           const std::function<void(T&)>& jacobian_fn = nullptr) {
         const size_t M = r.size();
         int32_t status = Failed;
         if (M < (size_t)nu) return {Non_Suff_Points, -1.0};
@@ -414,6 +415,7 @@ struct Optimizer {
         uint32_t n_proj = 0, pre_n_proj = 0;
         double lambda = 1e-2, nuf = 2.0;
         reset_all();
+        if (jacobian_fn) std::fill(J.begin(), J.end(), 0.0);  // resetAllParameters(computeJacobian = true)
         n_proj = residual_fn(params);
         tukey_weighting(n_proj);
         chi = chi2();
@@ -426,6 +428,7 @@ struct Optimizer {
                 pre_params = params; pre_chi = chi; pre_r = r; pre_w = w; pre_vis = vis; pre_n_proj = n_proj;
                 status = Success;
             }
+            if (jacobian_fn) jacobian_fn(params);  // :242-243
             normal_equations();
             if (cur_iter == 0) {
                 double mx = H[0];
@@ -874,6 +877,63 @@ static int32_t update_seed(const Camera& cam, const Image& kf_im, const SE3& kf_
     return kDepthUpdated;
 }
 
+// ------------------------------------------------------------------ pose-only bundle adjustment
+// BundleAdjustment::optimizePose (src/bundle_adjustment.cpp:35-69) with computeJacobianPose (:71-98),
+// computeResidualsPose (:101-134), computeImageJacPose (:136-160), updatePose (:162-166),
+// resetParameters (:306-309).  ref_vis is the member m_refVisibility: the residual functor runs before
+// the Jacobian functor in optimizeLM (src/optimizer.cpp:199 vs :242), so it reads the visibility the
+// PREVIOUS call's Jacobian functor left (all false on a fresh object).  Returns -1 where the reference
+// would dereference a null point (a stale visible flag on a feature without one).
+struct PoseBA {
+    Optimizer opt{6};
+    int32_t optimize_pose(int32_t n, const double* bearing, const double* point, const uint8_t* has_point,
+                          std::vector<uint8_t>& ref_vis, SE3& pose, double* err, int32_t* status) {
+        if (n == 0) { *err = 0.0; *status = -1; return 0; }          // :37-38 (no optimisation run)
+        opt.init_parameters((size_t)n * 3);                           // :45
+        ref_vis.resize(n, 0);                                         // :46
+        for (int32_t k = 0; k < n; ++k)
+            if (ref_vis[k] && !has_point[k]) return -1;
+        SE3 absolute = pose;
+        auto resid = [&](SE3& T) -> uint32_t {
+            uint32_t cnt = 0;
+            for (int32_t k = 0; k < n; ++k) {
+                if (!ref_vis[k]) continue;
+                const V3 pc = act(T, {point[3 * k], point[3 * k + 1], point[3 * k + 2]});
+                const double sq = pc.x * pc.x + pc.y * pc.y + pc.z * pc.z;  // Eigen normalized()
+                const V3 u = sq > 0.0 ? V3{pc.x / std::sqrt(sq), pc.y / std::sqrt(sq), pc.z / std::sqrt(sq)} : pc;
+                const V3 e{bearing[3 * k] - u.x, bearing[3 * k + 1] - u.y, bearing[3 * k + 2] - u.z};
+                opt.r[cnt++] = std::fabs(e.x);
+                opt.r[cnt++] = std::fabs(e.y);
+                opt.r[cnt] = std::fabs(e.z);
+                opt.vis[cnt] = 1;                                     // only the third row is visible (:127)
+                cnt++;
+            }
+            return cnt;
+        };
+        auto jac = [&](SE3& T) {
+            std::fill(ref_vis.begin(), ref_vis.end(), 0);             // resetParameters
+            uint32_t cp = 0;
+            for (int32_t k = 0; k < n; ++k) {
+                if (!has_point[k]) continue;
+                ref_vis[k] = 1;
+                const V3 X = act(T, {point[3 * k], point[3 * k + 1], point[3 * k + 2]});
+                const double Jr[3][6] = {{1.0, 0.0, 0.0, 0.0, X.z, -X.y},
+                                         {0.0, 1.0, 0.0, -X.z, 0.0, X.x},
+                                         {0.0, 0.0, 1.0, X.y, -X.x, 0.0}};
+                for (int i = 0; i < 3; ++i)
+                    for (int j = 0; j < 6; ++j) opt.J[(3 * cp + i) * 6 + j] = Jr[i][j];
+                cp++;
+            }
+        };
+        auto upd = [](SE3& T, const double* dx) { T = compose(se3_exp(dx), T); };  // exp(dx) * pose
+        auto res = opt.optimize_lm<SE3>(absolute, resid, upd, jac);
+        pose = absolute;                                              // :64 (unchanged on Non_Suff_Points)
+        *err = res.second;
+        *status = res.first;
+        return 0;
+    }
+};
+
 }  // namespace oracle
 
 // =====================================================================================================
@@ -1205,6 +1265,23 @@ int32_t oracle_stream_g6(double v, char* buf, int32_t cap) {
     if ((int32_t)s.size() + 1 > cap) return -1;
     std::memcpy(buf, s.c_str(), s.size() + 1);
     return (int32_t)s.size();
+}
+
+// BundleAdjustment::optimizePose on one frame: n features (bearing n x 3, point n x 3, has_point n);
+// vis_inout: m_refVisibility of the BundleAdjustment object (n_vis_in entries in, n out: the caller
+// resizes like the member).  status -1: no optimisation ran (n == 0, return value 0).
+int32_t oracle_optimize_pose(int32_t n, const double* bearing, const double* point, const uint8_t* has_point,
+                             int32_t n_vis_in, uint8_t* vis_inout, double* pose_inout, int32_t median_mode,
+                             double* err, int32_t* status) {
+    PoseBA ba;
+    ba.opt.median_mode = median_mode;
+    std::vector<uint8_t> vis(vis_inout, vis_inout + n_vis_in);
+    SE3 T{{pose_inout[0], pose_inout[1], pose_inout[2], pose_inout[3]}, {pose_inout[4], pose_inout[5], pose_inout[6]}};
+    if (ba.optimize_pose(n, bearing, point, has_point, vis, T, err, status) != 0) return -1;
+    if (n > 0) std::copy(vis.begin(), vis.end(), vis_inout);
+    const double o[7] = {T.q.x, T.q.y, T.q.z, T.q.w, T.t.x, T.t.y, T.t.z};
+    std::copy(o, o + 7, pose_inout);
+    return 0;
 }
 
 }  // extern "C"

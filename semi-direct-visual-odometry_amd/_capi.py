@@ -94,6 +94,8 @@ _SIGNATURES = [
                                               c_void_p, c_void_p, P_i32]),
     ("svo_pose_matrix3x4_inverse", c_int32, [c_void_p, c_void_p]),
     ("svo_format_kitti_pose", c_int32, [c_void_p, ctypes.c_char_p, c_int32]),
+    ("svo_pose_optimize", c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p]),
 ]
 
 EXPORTED = [s[0] for s in _SIGNATURES]

@@ -719,3 +719,54 @@ class FeatureSelection:
                                                 ptr(resp), ctypes.byref(n)))
         self.occupancy_grid[:] = occ
         return self._emit(frame, px, resp, n.value)
+
+
+# ---------------------------------------------------------------- pose-only bundle adjustment
+def pose_optimize_batch(feat_off, bearing, point, has_point, vis, poses, ctx=None):
+    """svo_pose_optimize over arrays: frame f owns rows feat_off[f]:feat_off[f+1].  vis (uint8, in/out) and
+    poses ((F, 7), in/out) are updated in place; returns (err, status)."""
+    ctx = ctx or default_context()
+    feat_off = np.ascontiguousarray(feat_off, np.int32)
+    F = len(feat_off) - 1
+    for a, dt in ((vis, np.uint8), (poses, np.float64)):
+        if a.dtype != dt or not a.flags.c_contiguous:
+            raise ValueError("vis must be C-contiguous uint8 and poses C-contiguous float64")
+    bearing = np.ascontiguousarray(bearing, np.float64)
+    point = np.ascontiguousarray(point, np.float64)
+    has_point = np.ascontiguousarray(has_point, np.uint8)
+    err = np.zeros(F)
+    st = np.zeros(F, np.int32)
+    check(lib().svo_pose_optimize(ctx.handle, F, ptr(feat_off), ptr(bearing), ptr(point), ptr(has_point), ptr(vis),
+                                  ptr(poses), ptr(err), ptr(st)))
+    return err, st
+
+
+class BundleAdjustment:
+    """BundleAdjustment(camera, level, numParameters) — optimizePose (src/bundle_adjustment.cpp:30-166).
+
+    ref_visibility is the member m_refVisibility: optimizePose's residual step reads the flags the
+    previous call left (a fresh object returns NaN and moves nothing), see include/svo_c.h."""
+
+    def __init__(self, camera, level=0, num_parameters=6, ctx=None):
+        self.camera, self.level = camera, int(level)
+        self.ctx = ctx or default_context()
+        self.ref_visibility = np.zeros(0, np.uint8)
+        self.last_status = None
+
+    def optimize_pose(self, frame):
+        n = len(frame.features)
+        if n == 0:  # :37-38
+            return 0.0
+        vis = np.zeros(n, np.uint8)
+        k = min(n, len(self.ref_visibility))
+        vis[:k] = self.ref_visibility[:k]  # m_refVisibility.resize(n, false)
+        bearing = np.array([f.bearing_vec for f in frame.features], np.float64).reshape(n, 3)
+        has = np.array([f.point is not None for f in frame.features], np.uint8)
+        point = np.array([f.point.position if f.point is not None else (0.0, 0.0, 0.0) for f in frame.features],
+                         np.float64).reshape(n, 3)
+        poses = np.ascontiguousarray(frame.abs_pose, np.float64).reshape(1, 7).copy()
+        err, st = pose_optimize_batch([0, n], bearing, point, has, vis, poses, self.ctx)
+        self.ref_visibility = vis
+        frame.abs_pose = poses[0].copy()
+        self.last_status = int(st[0])
+        return float(err[0])

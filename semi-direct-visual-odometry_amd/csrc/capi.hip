@@ -957,4 +957,62 @@ int svo_format_kitti_pose(const double* pose, char* buf, int32_t cap) {
     return SVO_OK;
 }
 
+// ------------------------------------------------------------------ pose-only bundle adjustment
+int svo_pose_optimize(svo_ctx* c, int32_t n_frames, const int32_t* feat_off, const double* bearing, const double* point,
+                      const uint8_t* has_point, uint8_t* vis_inout, double* poses_inout, double* err, int32_t* status) {
+    if (!c || (n_frames > 0 && (!feat_off || !poses_inout || !err || !status))) return fail(SVO_ERR_ARG, "null argument");
+    if (n_frames < 0) return fail(SVO_ERR_ARG, "n_frames < 0");
+    if (n_frames == 0) return SVO_OK;
+    if (feat_off[0] != 0) return fail(SVO_ERR_ARG, "feat_off[0] must be 0");
+    for (int32_t f = 0; f < n_frames; ++f)
+        if (feat_off[f + 1] < feat_off[f]) return fail(SVO_ERR_ARG, "feat_off not ascending at frame %d", f);
+    const int64_t nf = feat_off[n_frames];
+    if (nf > 0 && (!bearing || !point || !has_point || !vis_inout)) return fail(SVO_ERR_ARG, "null argument");
+    if (nf >= ((int64_t)1 << 28)) return fail(SVO_ERR_ARG, "too many features");
+    for (int64_t k = 0; k < nf; ++k)
+        if (vis_inout[k] && !has_point[k])
+            return fail(SVO_ERR_ARG, "feature %lld: visible from the previous call but without a point "
+                                     "(the reference dereferences a null m_point)", (long long)k);
+    SVO_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    // one scratch block: offsets | poses in | poses out | err | status | bearing | point | rows | wts | flags
+    const size_t F = (size_t)n_frames, N = (size_t)nf;
+    const size_t bytes = (F + 1) * 4 + 8 + F * 7 * 8 * 2 + F * 8 + F * 4 + 8 + N * 3 * 8 * 2 + N * 3 * 8 + N * 8 + N * 3 + 64;
+    void* base = nullptr;
+    hipError_t e = ctx_scratch(c, bytes, &base);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_pose_optimize: %s", hipGetErrorString(e));
+    char* q = static_cast<char*>(base);
+    auto take = [&](size_t b) { char* r = q; q += (b + 7) / 8 * 8; return r; };
+    int32_t* d_off = reinterpret_cast<int32_t*>(take((F + 1) * 4));
+    double* d_pin = reinterpret_cast<double*>(take(F * 7 * 8));
+    double* d_pout = reinterpret_cast<double*>(take(F * 7 * 8));
+    double* d_err = reinterpret_cast<double*>(take(F * 8));
+    int32_t* d_st = reinterpret_cast<int32_t*>(take(F * 4));
+    double* d_bear = reinterpret_cast<double*>(take(N * 3 * 8));
+    double* d_pt = reinterpret_cast<double*>(take(N * 3 * 8));
+    double* d_rows = reinterpret_cast<double*>(take(N * 3 * 8));
+    double* d_wts = reinterpret_cast<double*>(take(N * 8));
+    uint8_t* d_has = reinterpret_cast<uint8_t*>(take(N));
+    uint8_t* d_vin = reinterpret_cast<uint8_t*>(take(N));
+    uint8_t* d_vout = reinterpret_cast<uint8_t*>(take(N));
+    e = hipMemcpyAsync(d_off, feat_off, (F + 1) * 4, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_pin, poses_inout, F * 7 * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && N) e = hipMemcpyAsync(d_bear, bearing, N * 3 * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && N) e = hipMemcpyAsync(d_pt, point, N * 3 * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && N) e = hipMemcpyAsync(d_has, has_point, N, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess && N) e = hipMemcpyAsync(d_vin, vis_inout, N, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        svo::PoseBAArgs a{d_off, d_bear, d_pt, d_has, d_vin, d_vout, d_pin, d_pout, d_err, d_st, d_rows, d_wts, n_frames};
+        svo::launch_pose_ba(a, s);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(poses_inout, d_pout, F * 7 * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(err, d_err, F * 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(status, d_st, F * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && N) e = hipMemcpyAsync(vis_inout, d_vout, N, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_pose_optimize: %s", hipGetErrorString(e));
+    return SVO_OK;
+}
+
 }  // extern "C"

@@ -105,6 +105,23 @@ struct DepthArgs {
 };
 void launch_depth_update(const DepthArgs& a, hipStream_t s);
 
+struct PoseBAArgs {  // BundleAdjustment::optimizePose over a batch of frames (pose_ba.hip)
+    const int32_t* feat_off;    // [n_frames + 1] feature range of each frame
+    const double* bearing;      // [n_feat][3]
+    const double* point;        // [n_feat][3] world position of the feature's point (any if none)
+    const uint8_t* has_point;   // [n_feat]
+    const uint8_t* vis_in;      // [n_feat] m_refVisibility before the call
+    uint8_t* vis_out;           // [n_feat] after
+    const double* poses;        // [n_frames][7]
+    double* poses_out;          // [n_frames][7]
+    double* err;                // [n_frames]
+    int32_t* status;            // [n_frames]
+    double* rows;               // scratch [3 * n_feat]
+    double* wts;                // scratch [n_feat]
+    int32_t n_frames;
+};
+void launch_pose_ba(const PoseBAArgs& a, hipStream_t s);
+
 // FeatureSelection (feature_select.hip)
 int feature_detect_segments(int64_t npx);
 void launch_feature_detect(const uint8_t* plane, int width, int height, int thr, int* seg_counts, uint32_t* keys,

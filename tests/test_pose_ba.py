@@ -1,0 +1,208 @@
+"""Pose-only bundle adjustment: BundleAdjustment::optimizePose
+(src/bundle_adjustment.cpp:35-166) — one LM step of Optimizer::optimizeLM<SE3d> (src/optimizer.cpp:162-370).
+
+CPU: the oracle restatement (oracle/svo_oracle.cpp PoseBA, exact order statistics = median_mode 1) against
+an independent numpy/scipy restatement of the step (np.sort order statistics, numpy normal equations,
+np.linalg.solve, scipy rotations for SE3 exp), plus known answers and the reference's stateful quirks
+(m_refVisibility read before it is set: a fresh object returns NaN and moves nothing; Non_Suff_Points for
+one feature; 0 for no features; a stale flag on a feature without a point is an error).
+GPU: svo_amd.pose_optimize_batch (one workgroup per frame) and svo_amd.BundleAdjustment against the oracle:
+status and visibility equal, pose within 1e-12, RMSE within 1e-12 relative (the normal-equation sums run
+in a different order; every other step is the same arithmetic).
+"""
+import numpy as np
+import pytest
+from scipy.spatial.transform import Rotation
+
+import oracle as O
+
+DBL_MAX = np.finfo(np.float64).max
+
+
+def se3_exp(xi):
+    up, om = xi[:3], xi[3:]
+    th = np.linalg.norm(om)
+    W = np.array([[0, -om[2], om[1]], [om[2], 0, -om[0]], [-om[1], om[0], 0]])
+    if th < 1e-10:
+        V = np.eye(3) + 0.5 * W
+    else:
+        V = np.eye(3) + (1 - np.cos(th)) / th ** 2 * W + (th - np.sin(th)) / th ** 3 * (W @ W)
+    return Rotation.from_rotvec(om), V @ up
+
+
+def act(pose, P):
+    return Rotation.from_quat(pose[:4]).apply(P) + pose[4:]
+
+
+def py_optimize_pose(bearing, point, has, vis_in, pose):
+    """numpy restatement of optimizePose (exact medians)."""
+    n = len(has)
+    if n == 0:
+        return pose.copy(), 0.0, -1, np.array(vis_in, np.uint8)
+    vis = np.zeros(n, np.uint8)
+    k = min(n, len(vis_in))
+    vis[:k] = np.asarray(vis_in, np.uint8)[:k]
+    M = 3 * n
+    if M < 6:
+        return pose.copy(), -1.0, 6, vis
+    rows = np.full(M, DBL_MAX)
+    idx = np.nonzero(vis)[0]
+    pc = act(pose, point[idx])
+    u = pc / np.linalg.norm(pc, axis=1, keepdims=True)
+    e = np.abs(bearing[idx] - u)
+    rows[: 3 * len(idx)] = e.ravel()
+    n_proj = 3 * len(idx)
+
+    def median(v):
+        s = np.sort(v)
+        mid = n_proj // 2
+        return s[mid] if (M % 2 or mid == 0) else (s[mid - 1] + s[mid]) / 2.0
+
+    med = median(rows)
+    mad = median(np.abs(rows - med))
+    sigma = max(1.482602218505602 * mad, np.finfo(np.float64).eps)
+    c = 4.6851 * sigma
+    rz = rows[2: 3 * len(idx): 3]
+    w = np.where(np.abs(rz) <= c, (1 - rz * rz / (c * c)) ** 2, 0.0)
+    chi = float(np.sum(rz * rz * w))
+    pts = np.nonzero(has)[0]
+    X = act(pose, point[pts])[: len(idx)]
+    J = np.zeros((len(X), 6))
+    J[:, 2] = 1.0
+    J[:, 3] = X[:, 1]
+    J[:, 4] = -X[:, 0]
+    wj = w[: len(X)]
+    H = J.T @ (J * wj[:, None])
+    g = J.T @ (wj * rz[: len(X)])
+    lam = 1e-2 * np.max(np.diag(H))
+    A = H + lam * np.eye(6)
+    dx = np.linalg.solve(A, g) if lam > 0 else np.zeros(6)
+    R, t = se3_exp(dx)
+    q = (R * Rotation.from_quat(pose[:4])).as_quat()
+    q = q if np.dot(q, pose[:4]) >= 0 else -q
+    tn = R.apply(pose[4:]) + t
+    step = float(dx @ dx)
+    st = 3 if step < 1e-16 else 0
+    err = np.sqrt(chi / n_proj) if n_proj else float("nan")
+    return np.concatenate([q, tn]), err, st, has.astype(np.uint8)
+
+
+def scene(seed, n, null_frac=0.15, noise=2e-3, pose_err=0.02):
+    rng = np.random.default_rng(seed)
+    P = rng.normal(size=(n, 3)) * [4, 2, 3] + [0, 0, 12]
+    true = np.array([0, 0, 0, 1, 0.3, -0.1, 0.5])
+    q = Rotation.from_rotvec(rng.normal(size=3) * 0.05).as_quat()
+    true[:4] = q
+    pc = act(true, P)
+    b = pc / np.linalg.norm(pc, axis=1, keepdims=True) + rng.normal(size=(n, 3)) * noise
+    b /= np.linalg.norm(b, axis=1, keepdims=True)
+    has = (rng.random(n) > null_frac).astype(np.uint8)
+    init = true.copy()
+    init[:4] = (Rotation.from_rotvec(rng.normal(size=3) * pose_err) * Rotation.from_quat(q)).as_quat()
+    init[4:] += rng.normal(size=3) * pose_err
+    return b, P, has, init
+
+
+def canon(p):
+    p = np.array(p, np.float64)
+    return p if p[3] >= 0 else np.concatenate([-p[:4], p[4:]])
+
+
+# ---------------------------------------------------------------- CPU: oracle pinned
+@pytest.mark.parametrize("seed,n", [(0, 50), (1, 51), (2, 400), (3, 2), (4, 3), (5, 1000)])
+def test_oracle_matches_numpy_restatement(seed, n):
+    b, P, has, init = scene(seed, n)
+    vis0 = has.copy()  # a second call on the same frame: the previous Jacobian step left has_point
+    p_o, e_o, s_o, v_o = O.optimize_pose(b, P, has, vis0, init)
+    p_n, e_n, s_n, v_n = py_optimize_pose(b, P, has, vis0, init)
+    assert s_o == s_n
+    np.testing.assert_array_equal(v_o, v_n)
+    np.testing.assert_allclose(canon(p_o), canon(p_n), atol=1e-12)
+    assert abs(e_o - e_n) <= 1e-12 * abs(e_n)
+
+
+def test_fresh_object_returns_nan_and_keeps_pose():
+    b, P, has, init = scene(6, 40)
+    p, e, s, v = O.optimize_pose(b, P, has, [], init)
+    assert np.isnan(e) and s == 3  # Small_Step_Size: H = 0, dx = 0
+    np.testing.assert_allclose(p, init, atol=1e-15)
+    np.testing.assert_array_equal(v, has)
+
+
+def test_edge_cases():
+    b, P, has, init = scene(7, 5)
+    p, e, s, v = O.optimize_pose(b[:0], P[:0], has[:0], [1, 1], init)
+    assert (e, s) == (0.0, -1) and list(v) == [1, 1]
+    p, e, s, v = O.optimize_pose(b[:1], P[:1], np.ones(1, np.uint8), [1, 0, 1], init)
+    assert (e, s) == (-1.0, 6) and list(v) == [1]
+    np.testing.assert_array_equal(p, init)
+    with pytest.raises(ValueError):
+        O.optimize_pose(b, P, np.array([1, 0, 1, 1, 1], np.uint8), [1, 1, 0, 0, 0], init)
+
+
+def test_known_answer_exact_bearings():
+    b, P, has, init = scene(8, 60, noise=0.0, pose_err=0.0)
+    pc = act(init, P)
+    b = pc / np.linalg.norm(pc, axis=1, keepdims=True)
+    p, e, s, v = O.optimize_pose(b, P, has, has, init)
+    assert e < 1e-15 and s == 3
+    np.testing.assert_allclose(canon(p), canon(init), atol=1e-15)
+
+
+# ---------------------------------------------------------------- GPU parity
+def _batch(specs):
+    bs, Ps, hs, vs, poses, offs = [], [], [], [], [], [0]
+    for seed, n, stale in specs:
+        b, P, has, init = scene(seed, n)
+        vis = has.copy() if stale == "has" else np.zeros(n, np.uint8)
+        bs.append(b); Ps.append(P); hs.append(has); vs.append(vis); poses.append(init)
+        offs.append(offs[-1] + n)
+    cat = lambda xs, shape: np.concatenate(xs).reshape(shape) if offs[-1] else np.zeros(shape)
+    return (np.array(offs, np.int32), cat(bs, (-1, 3)), cat(Ps, (-1, 3)), np.concatenate(hs).astype(np.uint8),
+            np.concatenate(vs).astype(np.uint8), np.array(poses))
+
+
+@pytest.mark.gpu
+def test_gpu_batch_matches_oracle():
+    import svo_amd
+    specs = [(10, 50, "has"), (11, 51, "has"), (12, 2000, "has"), (13, 0, "has"), (14, 1, "has"), (15, 2, "has"),
+             (16, 3, "has"), (17, 300, "none"), (18, 777, "has"), (19, 4096, "has")]
+    off, b, P, has, vis, poses = _batch(specs)
+    vis_g = vis.copy()
+    poses_g = np.ascontiguousarray(poses.copy())
+    err, st = svo_amd.pose_optimize_batch(off, b, P, has, vis_g, poses_g)
+    for f in range(len(specs)):
+        s, e = off[f], off[f + 1]
+        p_o, e_o, s_o, v_o = O.optimize_pose(b[s:e], P[s:e], has[s:e], vis[s:e], poses[f])
+        assert st[f] == s_o, f
+        np.testing.assert_array_equal(vis_g[s:e], v_o)
+        np.testing.assert_allclose(canon(poses_g[f]), canon(p_o), atol=1e-12)
+        if np.isnan(e_o):
+            assert np.isnan(err[f])
+        else:
+            assert abs(err[f] - e_o) <= 1e-12 * max(abs(e_o), 1e-300), (f, err[f], e_o)
+
+
+@pytest.mark.gpu
+def test_gpu_bundle_adjustment_object_sequence():
+    """Two optimizePose calls on one object: NaN first (stale flags), then a real step — as the oracle."""
+    import svo_amd
+    b, P, has, init = scene(20, 300)
+    cam = svo_amd.PinholeCamera.kitti()
+    fr = svo_amd.Frame(cam, np.zeros((cam.height, cam.width), np.uint8), 1)
+    fr.abs_pose = init.copy()
+    for k in range(len(has)):
+        f = svo_amd.Feature(fr, np.zeros(2), bearing=b[k])
+        if has[k]:
+            f.point = svo_amd.Point(P[k])
+        fr.add_feature(f)
+    ba = svo_amd.BundleAdjustment(cam)
+    e1 = ba.optimize_pose(fr)
+    p1, o1, s1, v1 = O.optimize_pose(b, P, has, [], init)
+    assert np.isnan(e1) and np.isnan(o1) and ba.last_status == s1
+    np.testing.assert_allclose(canon(fr.abs_pose), canon(p1), atol=1e-12)
+    e2 = ba.optimize_pose(fr)
+    p2, o2, s2, v2 = O.optimize_pose(b, P, has, v1, p1)
+    assert ba.last_status == s2 and abs(e2 - o2) <= 1e-12 * o2
+    np.testing.assert_allclose(canon(fr.abs_pose), canon(p2), atol=1e-12)
+    np.testing.assert_array_equal(ba.ref_visibility, v2)
