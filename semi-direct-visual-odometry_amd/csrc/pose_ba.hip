@@ -1,6 +1,6 @@
 // pose_ba.hip — BundleAdjustment::optimizePose (src/bundle_adjustment.cpp:35-166) for a batch of frames.
 //
-// One 256-thread workgroup per frame runs the reference's single LM step (Optimizer::optimizeLM<SE3d>,
+// One 512-thread workgroup per frame runs the reference's single LM step (Optimizer::optimizeLM<SE3d>,
 // src/optimizer.cpp:162-370, which always leaves after the first damped step):
 //   residuals  computeResidualsPose (:101-134) for the features the PREVIOUS call's Jacobian functor
 //              marked visible (m_refVisibility, carried by the caller): |bearing - normalise(T P)| as
@@ -24,7 +24,7 @@ namespace svo {
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 512;
 
 __device__ __forceinline__ uint64_t dbits(double v) { return (uint64_t)__double_as_longlong(v); }
 
@@ -69,13 +69,40 @@ __device__ double select_kth(const double* rows, int m, double med, uint32_t k, 
     return __longlong_as_double((long long)prefix);
 }
 
-// algorithm::computeMedian over m rows with n_valid (odd / even by the total length; exact neighbour)
+// algorithm::computeMedian over m rows with n_valid (odd / even by the total length; exact neighbour).
+// The neighbour below rank mid is hi itself when fewer than mid rows are smaller, else the largest
+// smaller row: one counting pass instead of a second selection.
 template <bool kMad>
 __device__ double median_rows(const double* rows, int m, double med, uint32_t n_valid, uint32_t* hist, uint64_t* sh) {
     const uint32_t mid = n_valid / 2;
     const double hi = select_kth<kMad>(rows, m, med, mid, hist, sh);
     if ((m & 1) || mid == 0) return hi;
-    const double lo = select_kth<kMad>(rows, m, med, mid - 1, hist, sh);
+    const uint64_t hk = dbits(hi);
+    uint32_t less = 0;
+    uint64_t below = 0;
+    for (int i = threadIdx.x; i < m; i += kThreads) {
+        const uint64_t key = dbits(kMad ? fabs(rows[i] - med) : rows[i]);
+        if (key < hk) {
+            ++less;
+            below = key > below ? key : below;
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        less += __shfl_xor(less, d, 64);
+        const uint64_t o = (uint64_t)__shfl_xor((long long)below, d, 64);
+        below = o > below ? o : below;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        hist[threadIdx.x >> 6] = less;
+        sh[0] = 0;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicMax((unsigned long long*)&sh[0], (unsigned long long)below);
+    __syncthreads();
+    uint32_t cnt = 0;
+    for (int w = 0; w < kThreads / 64; ++w) cnt += hist[w];
+    const double lo = cnt == mid ? __longlong_as_double((long long)sh[0]) : hi;
+    __syncthreads();
     return (lo + hi) / 2.0;
 }
 
@@ -118,7 +145,8 @@ __global__ void __launch_bounds__(kThreads) pose_ba_kernel(PoseBAArgs a) {
         __syncthreads();
         int before = nvis;
         for (int w = 0; w < wave; ++w) before += scan_sh[w];
-        const int chunk = scan_sh[0] + scan_sh[1] + scan_sh[2] + scan_sh[3];
+        int chunk = 0;
+        for (int w = 0; w < kThreads / 64; ++w) chunk += scan_sh[w];
         if (v) {
             const int j = before + inc - 1;
             const V3 pc = se3_act(T, {point[3 * k], point[3 * k + 1], point[3 * k + 2]});
@@ -172,7 +200,8 @@ __global__ void __launch_bounds__(kThreads) pose_ba_kernel(PoseBAArgs a) {
         __syncthreads();
         int before = cp_base;
         for (int w = 0; w < wave; ++w) before += scan_sh[w];
-        const int chunk = scan_sh[0] + scan_sh[1] + scan_sh[2] + scan_sh[3];
+        int chunk = 0;
+        for (int w = 0; w < kThreads / 64; ++w) chunk += scan_sh[w];
         if (k < n) a.vis_out[off + k] = (uint8_t)v;  // resetParameters + the Jacobian functor's flags
         if (v) {
             const int cp = before + inc - 1;
@@ -204,7 +233,10 @@ __global__ void __launch_bounds__(kThreads) pose_ba_kernel(PoseBAArgs a) {
     __syncthreads();
     if (threadIdx.x != 0) return;
     double s[28];
-    for (int i = 0; i < 28; ++i) s[i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    for (int i = 0; i < 28; ++i) {
+        s[i] = red[0][i];
+        for (int w = 1; w < kThreads / 64; ++w) s[i] += red[w][i];
+    }
     double H[36], g[6], dx[6];
     int t = 0;
     for (int i = 0; i < 6; ++i)
