@@ -10,6 +10,7 @@ plus the batched forms the GPU is built for (AlignBatch, FeatureAlignment.align_
 """
 import ctypes
 import math
+import time
 
 import numpy as np
 
@@ -473,6 +474,7 @@ class Map:
         self.candidates = []  # [feature, point, matched]
         self.alignment = FeatureAlignment(7, 0, 3, ctx)
         self.key_frames = []
+        self.native_seconds = 0.0  # time inside the C ABI calls (plan, projection, batched alignment)
 
     def cell_of(self, px):
         return int(px[1]) // self.cell_size * self.grid_cols + int(px[0]) // self.cell_size
@@ -502,12 +504,14 @@ class Map:
         sel_px = np.zeros((n_cells, 2))
         n_sel, m, t = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         cam = self.camera.as_c()
+        t0 = time.perf_counter()
         check(lib().svo_map_reproject_plan(ctypes.byref(cam), self.cell_size, n_cells, ptr(self.cell_orders),
                                            ptr(np.ascontiguousarray(cur_frame.abs_pose, np.float64)),
                                            ctypes.c_uint64(cur_frame.id), len(kfs), ptr(off), ptr(feat_point), npt,
                                            ptr(pos), ptr(ptype), ptr(plast), ptr(overlap), ctypes.byref(n_sel),
                                            ptr(sel_feat), ptr(sel_cell), ptr(sel_px), ctypes.byref(m),
                                            ctypes.byref(t)))
+        self.native_seconds += time.perf_counter() - t0
         for p, last in zip(points, plast):
             p.last_projected_kf_id = int(last)
         for k, kf in enumerate(kfs):
@@ -516,7 +520,9 @@ class Map:
         ns = n_sel.value
         chosen = [feats[i] for i in sel_feat[:ns]]
         px = np.ascontiguousarray(sel_px[:ns])
+        t0 = time.perf_counter()
         self.alignment.align_many(chosen, cur_frame, px)
+        self.native_seconds += time.perf_counter() - t0
         for i, ref_feature in enumerate(chosen):  # :558-569
             point = ref_feature.point
             point.succeeded_projection += 1
@@ -535,7 +541,10 @@ class Map:
     def add_candidate_to_frame(self, frame):
         if not self.candidates:
             return
-        px0 = frame.world2image(np.array([c[1].position for c in self.candidates]))
+        pos = np.array([c[1].position for c in self.candidates])
+        t0 = time.perf_counter()
+        px0 = frame.world2image(pos)
+        self.native_seconds += time.perf_counter() - t0
         w, h = frame.camera.width, frame.camera.height
         elig, cells = [], []
         for i, q in enumerate(px0):
@@ -545,7 +554,10 @@ class Map:
                     elig.append(i)
                     cells.append(k)
         px = np.ascontiguousarray(px0[elig])
-        err, _ = self.alignment.align_many([self.candidates[i][0] for i in elig], frame, px)
+        cands = [self.candidates[i][0] for i in elig]
+        t0 = time.perf_counter()
+        err, _ = self.alignment.align_many(cands, frame, px)
+        self.native_seconds += time.perf_counter() - t0
         for j, i in enumerate(elig):  # the reference's order: a cell taken earlier in this loop is skipped
             if self.cell_visited[cells[j]] or not err[j] < 50.0:
                 continue
