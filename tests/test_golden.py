@@ -1,4 +1,4 @@
-"""Golden fixtures (tests/golden/, written by tests/golden/make_golden.py): the oracle must keep
+"""Golden fixtures (tests/golden/, written by tests/golden/make_golden*.py): the oracle must keep
 reproducing them exactly (CPU), and the HIP path must match them within the parity tolerances (GPU)."""
 import os
 
@@ -98,3 +98,70 @@ def test_gpu_matches_golden():
     px = np.ascontiguousarray(fd["init_px"].copy())
     err, st = svo_amd.FeatureAlignment(7).align_batch(ps2, 0, ps2, 1, fd["ref_px"], px, camera)
     assert np.array_equal(px, fd["px"]) and np.array_equal(st, fd["status"])
+
+
+# ---------------------------------------------------------------- FeatureSelection / pose BA fixtures
+# (tests/golden/make_golden_select_ba.py)
+def _sel():
+    return load("select_small.npz")
+
+
+def _ba():
+    return load("pose_ba_small.npz")
+
+
+def test_oracle_reproduces_golden_feature_selection():
+    d = _sel()
+    for name, bucket in (("b", True), ("nb", False)):
+        px, resp, occ, nk = O.feature_select_ssc(d["img"], 40, 60, bucket, 16, d["occ"])
+        np.testing.assert_array_equal(px, d[f"ssc_{name}_px"])
+        np.testing.assert_array_equal(resp, d[f"ssc_{name}_resp"])
+        np.testing.assert_array_equal(occ, d[f"ssc_{name}_occ"])
+        assert nk == int(d[f"ssc_{name}_nk"])
+    px, resp, _ = O.feature_select_by_value(d["img"], 40, 16, d["occ"])
+    np.testing.assert_array_equal(px, d["val_px"])
+    np.testing.assert_array_equal(resp, d["val_resp"])
+
+
+def test_oracle_reproduces_golden_pose_ba():
+    d = _ba()
+    p1, e1, s1, v1 = O.optimize_pose(d["bearing"], d["point"], d["has_point"], [], d["init"])
+    assert np.isnan(e1) and np.isnan(d["err1"]) and s1 == d["status1"]
+    np.testing.assert_array_equal(p1, d["pose1"])
+    np.testing.assert_array_equal(v1, d["vis1"])
+    p2, e2, s2, v2 = O.optimize_pose(d["bearing"], d["point"], d["has_point"], v1, p1)
+    assert e2 == d["err2"] and s2 == d["status2"]
+    np.testing.assert_array_equal(p2, d["pose2"])
+
+
+@pytest.mark.gpu
+def test_gpu_matches_golden_feature_selection_and_pose_ba():
+    import svo_amd
+    d = _sel()
+    h, w = d["img"].shape
+    cam = svo_amd.PinholeCamera(w, h, 100.0, 100.0, w / 2, h / 2)
+    for name, bucket in (("b", True), ("nb", False)):
+        fr = svo_amd.Frame(cam, d["img"], 1)
+        fs = svo_amd.FeatureSelection(w, h, 16)
+        fs.occupancy_grid[:] = d["occ"]
+        fs.gradient_magnitude_with_ssc(fr, 40, 60, bucket)
+        np.testing.assert_array_equal(np.array([f.pixel_position for f in fr.features]).reshape(-1, 2),
+                                      d[f"ssc_{name}_px"])
+        np.testing.assert_array_equal([f.gradient_magnitude for f in fr.features], d[f"ssc_{name}_resp"])
+        np.testing.assert_array_equal(fs.occupancy_grid, d[f"ssc_{name}_occ"])
+    fr = svo_amd.Frame(cam, d["img"], 1)
+    fs = svo_amd.FeatureSelection(w, h, 16)
+    fs.occupancy_grid[:] = d["occ"]
+    fs.gradient_magnitude_by_value(fr, 40)
+    np.testing.assert_array_equal(np.array([f.pixel_position for f in fr.features]).reshape(-1, 2), d["val_px"])
+    b = _ba()
+    n = len(b["has_point"])
+    vis = np.zeros(n, np.uint8)
+    poses = b["init"].reshape(1, 7).copy()
+    err, st = svo_amd.pose_optimize_batch([0, n], b["bearing"], b["point"], b["has_point"], vis, poses)
+    assert np.isnan(err[0]) and st[0] == b["status1"]
+    np.testing.assert_array_equal(vis, b["vis1"])
+    np.testing.assert_allclose(poses[0], b["pose1"], atol=1e-12)
+    err, st = svo_amd.pose_optimize_batch([0, n], b["bearing"], b["point"], b["has_point"], vis, poses)
+    assert st[0] == b["status2"] and abs(err[0] - b["err2"]) <= 1e-12 * b["err2"]
+    np.testing.assert_allclose(poses[0], b["pose2"], atol=1e-12)
