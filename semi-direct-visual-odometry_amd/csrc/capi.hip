@@ -203,6 +203,7 @@ int svo_pyramid_set_create(svo_ctx* c, int32_t n_frames, int32_t width, int32_t 
     *out = nullptr;
     if (n_frames <= 0 || width < 3 || height < 3 || levels < 1 || levels > svo::kMaxLevels)
         return fail(SVO_ERR_ARG, "bad pyramid geometry n=%d %dx%d levels=%d", n_frames, width, height, levels);
+    if (width > 4096) return fail(SVO_ERR_ARG, "width %d > 4096 (the gradient kernel stages two rows per run)", width);
     SVO_HIP(hipSetDevice(c->device));
     svo_pyramid_set* p = new (std::nothrow) svo_pyramid_set{};
     if (!p) return fail(SVO_ERR_ARG, "out of host memory");
