@@ -95,6 +95,8 @@ def main():
     ps.build()
     ctx.record(3)
     pyr_ms = ctx.elapsed_ms(2, 3)
+    pyr_bytes = 2 * cam["width"] * cam["height"] + 2 * (level_bytes(cam["width"], cam["height"], L)
+                                                       - cam["width"] * cam["height"])
 
     batch = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx)
     for i in range(P):
@@ -161,7 +163,12 @@ def main():
                      "stages_ms": {k: round(v, 4) for k, v in stages.items()},
                      "dominant_stage": max(stages, key=stages.get)},
         "pyramid_build": {"frames": 3 * P, "ms": round(pyr_ms, 4),
-                          "frames_per_s": round(3 * P / (pyr_ms * 1e-3), 1)},
+                          "frames_per_s": round(3 * P / (pyr_ms * 1e-3), 1),
+                          # algorithmic bytes per frame: read the base image once, write the gradient
+                          # base and levels 1.. of both stacks (SURVEY 8(d) pyramid row)
+                          "algorithmic_bytes_per_frame": pyr_bytes,
+                          "achieved_GBps": round(3 * P * pyr_bytes / (pyr_ms * 1e-3) / 1e9, 1),
+                          "frac_hbm_peak": round(3 * P * pyr_bytes / (pyr_ms * 1e-3) / 8.0e12, 4)},
         "status_counts": {svo_amd.STATUS_NAMES[int(k)]: int(v) for k, v in zip(*np.unique(status, return_counts=True))},
     }
     if not args.no_secondary:

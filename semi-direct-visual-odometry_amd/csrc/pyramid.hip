@@ -6,20 +6,17 @@
 //                 gradient, not the gradient of the downsampled image): 5x5 [1 4 6 4 1]^2 kernel,
 //                 BORDER_REFLECT_101, (sum + 128) >> 8, dst size ((w+1)/2, (h+1)/2).
 // Integer arithmetic only, so the result is bit-exact by construction.  pyrDown: each 256-thread
-// workgroup computes a 64x16 destination tile from a (2*16+4)x(2*64+4) source tile staged in LDS
-// (reflection only for border tiles), separable horizontal then vertical pass.  Gradient: flat 4096-pixel
-// runs staged with 16-B loads, 16 pixels and one 16-B store per thread.
+// workgroup computes an 8x256 destination tile, vertical pass from global memory (a thread per source
+// column) into LDS, then the horizontal pass.  Gradient: flat
+// runs (8192 px) staged with 16-B loads, 16 pixels and one 16-B store per thread.
 #include "svo_internal.h"
 
 namespace svo {
 
 namespace {
 
-constexpr int kTileW = 64, kTileH = 16;
-constexpr int kSrcW = 2 * kTileW + 4, kSrcH = 2 * kTileH + 4;
-
-// BORDER_REFLECT_101 for i in [-2, n + 1] (the 5-tap footprint of a valid output); staged halo cells
-// that no output reads are clamped into the image so that every staged load stays in bounds.
+// BORDER_REFLECT_101 for i in [-2, n + 1] (the 5-tap footprint of a valid output); rows / columns that
+// no output reads are clamped into the image so that every load stays in bounds.
 __device__ __forceinline__ int reflect101(int i, int n) {
     if (n == 1) return 0;
     i = i < 0 ? -i : i;
@@ -27,51 +24,78 @@ __device__ __forceinline__ int reflect101(int i, int n) {
     return min(max(i, 0), n - 1);
 }
 
-// frames [first, first+count) x {intensity, gradient}; grid.z = 2*count.  Separable: the horizontal
-// [1 4 6 4 1] pass over the staged rows into LDS (16-bit sums), then the vertical pass.
+// frames [first, first+count) x {intensity, gradient}; grid.z = 2*count.  A workgroup makes an
+// 8-row x 256-column destination tile: vertical [1 4 6 4 1] pass first, one thread per source column
+// reading its 20 source rows straight from global memory (consecutive threads, consecutive bytes),
+// 16-bit column sums into LDS, then the horizontal pass from LDS.
+constexpr int kDnW = 256, kDnH = 8;
+constexpr int kDnCols = 2 * kDnW + 4, kDnRows = 2 * kDnH + 4;
+
 __global__ void __launch_bounds__(256) pyr_down_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
                                                        int64_t src_off, int sw, int sh, int64_t dst_off, int dw,
                                                        int dh, int first) {
-    __shared__ uint8_t tile[kSrcH][kSrcW];
-    __shared__ uint16_t hs[kSrcH][kTileW];
+    __shared__ uint16_t vs[kDnH][kDnCols];
     const int frame = first + (blockIdx.z >> 1);
     uint8_t* base = stacks + frame * frame_stride + ((blockIdx.z & 1) ? grad_off : 0);
     const uint8_t* src = base + src_off;
     uint8_t* dst = base + dst_off;
-    const int dx0 = blockIdx.x * kTileW, dy0 = blockIdx.y * kTileH;
+    const int dx0 = blockIdx.x * kDnW, dy0 = blockIdx.y * kDnH;
     const int sx0 = 2 * dx0 - 2, sy0 = 2 * dy0 - 2;
-    const bool interior = sx0 >= 0 && sy0 >= 0 && sx0 + kSrcW <= sw && sy0 + kSrcH <= sh;
-    for (int i = threadIdx.x; i < kSrcH * kSrcW; i += 256) {
-        const int ty = i / kSrcW, tx = i - ty * kSrcW;
-        const int y = interior ? sy0 + ty : reflect101(sy0 + ty, sh);
-        const int x = interior ? sx0 + tx : reflect101(sx0 + tx, sw);
-        tile[ty][tx] = src[(int64_t)y * sw + x];
+    const int nrows = min(kDnH, dh - dy0);                 // destination rows of this tile
+    const int ncols = min(2 * min(kDnW, dw - dx0) + 4, kDnCols);  // source columns the tile reads
+    int64_t roff[kDnRows];
+#pragma unroll
+    for (int r = 0; r < kDnRows; ++r) roff[r] = (int64_t)reflect101(sy0 + r, sh) * sw;
+    for (int c = threadIdx.x; c < ncols; c += 256) {
+        const int x = reflect101(sx0 + c, sw);
+        uint32_t v[kDnRows];
+#pragma unroll
+        for (int r = 0; r < kDnRows; ++r) v[r] = src[roff[r] + x];
+#pragma unroll
+        for (int t = 0; t < kDnH; ++t)
+            if (t < nrows)
+                vs[t][c] = (uint16_t)(v[2 * t] + 4 * v[2 * t + 1] + 6 * v[2 * t + 2] + 4 * v[2 * t + 3] + v[2 * t + 4]);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kSrcH * kTileW; i += 256) {
-        const int ty = i / kTileW, tx = i - ty * kTileW;
-        const uint8_t* r = tile[ty] + 2 * tx;
-        hs[ty][tx] = (uint16_t)(r[0] + 4 * r[1] + 6 * r[2] + 4 * r[3] + r[4]);
-    }
-    __syncthreads();
-    const int tx = threadIdx.x & (kTileW - 1);
-    for (int ty = threadIdx.x >> 6; ty < kTileH; ty += 4) {
-        const int x = dx0 + tx, y = dy0 + ty;
-        if (x >= dw || y >= dh) continue;
-        const int s = hs[2 * ty][tx] + 4 * hs[2 * ty + 1][tx] + 6 * hs[2 * ty + 2][tx] + 4 * hs[2 * ty + 3][tx] +
-                      hs[2 * ty + 4][tx];
-        dst[(int64_t)y * dw + x] = (uint8_t)((s + 128) >> 8);
+    const int x = dx0 + threadIdx.x;
+    if (x >= dw) return;
+    const int c = 2 * threadIdx.x;
+    for (int t = 0; t < nrows; ++t) {
+        const uint16_t* r = vs[t] + c;
+        const int s = r[0] + 4 * r[1] + 6 * r[2] + 4 * r[3] + r[4];
+        dst[(int64_t)(dy0 + t) * dw + x] = (uint8_t)((s + 128) >> 8);
     }
 }
 
-// Simd::AbsGradientSaturatedSum over a flat run of kGradRun pixels per workgroup: the run plus one row
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+__device__ __forceinline__ uint32_t grad4(uint32_t l, uint32_t r, uint32_t u, uint32_t d) {
+    uint32_t res = 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const u16x2 L = as_u16x2((l >> (8 * half)) & 0x00FF00FFu), R = as_u16x2((r >> (8 * half)) & 0x00FF00FFu);
+        const u16x2 Up = as_u16x2((u >> (8 * half)) & 0x00FF00FFu), Dn = as_u16x2((d >> (8 * half)) & 0x00FF00FFu);
+        const u16x2 gx = __builtin_elementwise_max(L, R) - __builtin_elementwise_min(L, R);
+        const u16x2 gy = __builtin_elementwise_max(Up, Dn) - __builtin_elementwise_min(Up, Dn);
+        const u16x2 g = __builtin_elementwise_min(gx + gy, (u16x2){255, 255});
+        res |= as_u32(g) << (8 * half);
+    }
+    return res;
+}
+
+// Simd::AbsGradientSaturatedSum over a flat run of kGradRun (8192) pixels per workgroup: the run plus one row
 // (and one pixel) either side is staged in LDS with 16-B loads, each thread forms 16 consecutive pixels
 // and writes them with one 16-B store.  Plane bases are 256-B aligned (make_geom), so the run is too.
-constexpr int kGradRun = 256 * 16;
+// Interior runs read aligned dwords and realign them with v_alignbyte; the four neighbours are combined
+// byte-parallel in 16-bit lanes.  Runs touching the border take a per-pixel path.
+constexpr int kGradThreads = 512;
+constexpr int kGradRun = kGradThreads * 16;
 constexpr int kGradMaxW = 4096;  // staged rows: the run + 2 rows + 2 px (+ 16-B rounding)
 constexpr int kGradStage = kGradRun + 2 * kGradMaxW + 64;
 
-__global__ void __launch_bounds__(256) abs_grad_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off, int w,
+__global__ void __launch_bounds__(kGradThreads) abs_grad_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off, int w,
                                                        int h, int first) {
     __shared__ __attribute__((aligned(16))) uint8_t st[kGradStage];
     const int frame = first + blockIdx.y;
@@ -85,25 +109,48 @@ __global__ void __launch_bounds__(256) abs_grad_kernel(uint8_t* stacks, int64_t 
     int64_t s1 = p0 + kGradRun + w + 1;
     s1 = s1 > npx ? npx : s1;
     const int64_t full = (s1 - s0) & ~(int64_t)15;  // 16-B chunks entirely inside the plane
-    for (int64_t o = (int64_t)threadIdx.x * 16; o < full; o += 256 * 16)
+    for (int64_t o = (int64_t)threadIdx.x * 16; o < full; o += kGradThreads * 16)
         *reinterpret_cast<uint4*>(st + o) = *reinterpret_cast<const uint4*>(src + s0 + o);
-    for (int64_t o = full + threadIdx.x; o < s1 - s0; o += 256) st[o] = src[s0 + o];
+    for (int64_t o = full + threadIdx.x; o < s1 - s0; o += kGradThreads) st[o] = src[s0 + o];
     __syncthreads();
     const int64_t q0 = p0 + (int64_t)threadIdx.x * 16;
     if (q0 >= npx) return;
-    int y = (int)(q0 / w), x = (int)(q0 - (int64_t)y * w);
-    uint32_t out[4] = {0, 0, 0, 0};
+    const int y = (int)(q0 / w), x = (int)(q0 - (int64_t)y * w);
     const int n = npx - q0 < 16 ? (int)(npx - q0) : 16;
-    for (int i = 0; i < n; ++i) {
-        uint32_t g = 0;
-        if (x > 0 && y > 0 && x < w - 1 && y < h - 1) {
-            const uint8_t* c = st + (q0 + i - s0);
-            const int gx = abs((int)c[1] - (int)c[-1]);
-            const int gy = abs((int)c[w] - (int)c[-w]);
-            g = (uint32_t)min(gx + gy, 255);
+    const int yl = (int)((q0 + n - 1) / w);
+    const int c0 = (int)(q0 - s0);  // 16-B aligned LDS offset of the run
+    uint32_t out[4];
+    if (n == 16 && y > 0 && yl < h - 1 && x > 0 && x + 15 < w - 1) {
+        // interior run of one row: aligned dword LDS reads realigned with v_alignbyte
+        const uint32_t* sd = reinterpret_cast<const uint32_t*>(st);
+        uint32_t C[6], U[5], D[5];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) C[i] = sd[c0 / 4 - 1 + i];
+        const int cu = c0 - w, cd = c0 + w;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            U[i] = sd[(cu >> 2) + i];
+            D[i] = sd[(cd >> 2) + i];
         }
-        out[i >> 2] |= g << (8 * (i & 3));
-        if (++x == w) { x = 0; ++y; }
+        const uint32_t su = (uint32_t)(cu & 3), sdn = (uint32_t)(cd & 3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            out[i] = grad4(__builtin_amdgcn_alignbyte(C[i + 1], C[i], 3), __builtin_amdgcn_alignbyte(C[i + 2], C[i + 1], 1),
+                           __builtin_amdgcn_alignbyte(U[i + 1], U[i], su), __builtin_amdgcn_alignbyte(D[i + 1], D[i], sdn));
+    } else {
+        int yy = y, xx = x;
+        out[0] = out[1] = out[2] = out[3] = 0;
+        for (int i = 0; i < n; ++i) {
+            uint32_t g = 0;
+            if (xx > 0 && yy > 0 && xx < w - 1 && yy < h - 1) {
+                const uint8_t* c = st + (c0 + i);
+                const int gx = abs((int)c[1] - (int)c[-1]);
+                const int gy = abs((int)c[w] - (int)c[-w]);
+                g = (uint32_t)min(gx + gy, 255);
+            }
+            out[i >> 2] |= g << (8 * (i & 3));
+            if (++xx == w) { xx = 0; ++yy; }
+        }
     }
     if (n == 16) {
         *reinterpret_cast<uint4*>(dst + q0) = make_uint4(out[0], out[1], out[2], out[3]);
@@ -120,10 +167,10 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
     const int64_t grad_off = (g.frame_bytes + 255) / 256 * 256;
     const int64_t stride = (grad_off + g.frame_bytes + 255) / 256 * 256;
     const int64_t npx = (int64_t)g.w[0] * g.h[0];
-    hipLaunchKernelGGL(abs_grad_kernel, dim3((unsigned)((npx + kGradRun - 1) / kGradRun), count), dim3(256), 0, s,
+    hipLaunchKernelGGL(abs_grad_kernel, dim3((unsigned)((npx + kGradRun - 1) / kGradRun), count), dim3(kGradThreads), 0, s,
                        stacks, stride, grad_off, g.w[0], g.h[0], first);
     for (int l = 1; l < g.levels; ++l) {
-        dim3 grid((g.w[l] + kTileW - 1) / kTileW, (g.h[l] + kTileH - 1) / kTileH, 2 * count);
+        dim3 grid((g.w[l] + kDnW - 1) / kDnW, (g.h[l] + kDnH - 1) / kDnH, 2 * count);
         hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, s, stacks, stride, grad_off, g.off[l - 1], g.w[l - 1],
                            g.h[l - 1], g.off[l], g.w[l], g.h[l], first);
     }
