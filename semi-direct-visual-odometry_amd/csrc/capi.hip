@@ -65,6 +65,9 @@ struct svo_ctx {
     // allocation per call once warm
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
+    // pinned host staging of the same calls (fixed size, ctx_pinned): one H2D and one D2H copy per call
+    void* pinned = nullptr;
+    size_t pinned_bytes = 0;
 };
 
 // at least `bytes` of the context's scratch (the previous contents are not kept)
@@ -79,6 +82,25 @@ static hipError_t ctx_scratch(svo_ctx* c, size_t bytes, void** out) {
         c->scratch_bytes = want;
     }
     *out = c->scratch;
+    return hipSuccess;
+}
+
+// the context's pinned host staging (kPinnedCap bytes, allocated once on first use and never resized:
+// measured on the MI355X boxes, copies into a pinned block allocated after a hipHostFree of the previous
+// one failed with "invalid argument").  Calls whose payload exceeds it (or when pinning fails) stage in
+// pageable memory or copy straight from the caller's arrays.
+constexpr size_t kPinnedCap = (size_t)8 << 20;
+static hipError_t ctx_pinned(svo_ctx* c, size_t bytes, void** out) {
+    if (bytes > kPinnedCap) return hipErrorInvalidValue;
+    if (!c->pinned) {
+        const hipError_t e = hipHostMalloc(&c->pinned, kPinnedCap, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            c->pinned = nullptr;
+            return e;
+        }
+        c->pinned_bytes = kPinnedCap;
+    }
+    *out = c->pinned;
     return hipSuccess;
 }
 
@@ -167,6 +189,7 @@ int svo_ctx_destroy(svo_ctx* c) {
         if (c->sides[i]) (void)hipStreamDestroy(c->sides[i]);
     }
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->pinned) (void)hipHostFree(c->pinned);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SVO_OK;
@@ -538,19 +561,32 @@ static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_s
                               double* px_inout, double* err, int32_t* status) {
     SVO_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    // one scratch block: ref planes | ref px | px | err | status (8-B aligned pieces)
+    // one block, same layout on both sides: ref planes | ref px | px | err | status (8-B aligned pieces);
+    // one H2D copy of the inputs (planes .. px) and one D2H copy of the outputs (px .. status)
     const size_t nn = (size_t)n;
+    const size_t in_bytes = nn * (sizeof(void*) + 4 * sizeof(double));
+    const size_t out_off = nn * (sizeof(void*) + 2 * sizeof(double));
+    const size_t total = nn * (sizeof(void*) + 5 * sizeof(double) + 8);
     void* base = nullptr;
-    hipError_t e = ctx_scratch(c, nn * (sizeof(void*) + 5 * sizeof(double) + 8), &base);
+    void* host = nullptr;
+    std::vector<char> pageable;  // staging past kPinnedCap
+    hipError_t e = ctx_scratch(c, total, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
+    if (ctx_pinned(c, total, &host) != hipSuccess) {
+        (void)hipGetLastError();
+        pageable.resize(total);
+        host = pageable.data();
+    }
+    char* hb = static_cast<char*>(host);
+    std::memcpy(hb, rg.data(), nn * sizeof(void*));
+    std::memcpy(hb + nn * sizeof(void*), ref_px, nn * 2 * sizeof(double));
+    std::memcpy(hb + out_off, px_inout, nn * 2 * sizeof(double));
     const uint8_t** d_rg = static_cast<const uint8_t**>(base);
     double* d_rpx = reinterpret_cast<double*>(d_rg + nn);
     double* d_px = d_rpx + 2 * nn;
     double* d_err = d_px + 2 * nn;
     int32_t* d_st = reinterpret_cast<int32_t*>(d_err + nn);
-    e = hipMemcpyAsync(d_rg, rg.data(), n * sizeof(void*), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_rpx, ref_px, n * 2 * sizeof(double), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_px, px_inout, n * 2 * sizeof(double), hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(base, hb, in_bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         svo::FeatureAlignArgs a;
         a.ref_grad = d_rg;
@@ -567,11 +603,13 @@ static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_s
         svo::launch_feature_align(a, s);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(px_inout, d_px, n * 2 * sizeof(double), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && err) e = hipMemcpyAsync(err, d_err, n * sizeof(double), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && status) e = hipMemcpyAsync(status, d_st, n * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(hb + out_off, static_cast<char*>(base) + out_off, total - out_off, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
+    std::memcpy(px_inout, hb + out_off, nn * 2 * sizeof(double));
+    if (err) std::memcpy(err, hb + out_off + nn * 2 * sizeof(double), nn * sizeof(double));
+    if (status) std::memcpy(status, hb + out_off + nn * 3 * sizeof(double), nn * sizeof(int32_t));
     return SVO_OK;
 }
 
@@ -746,51 +784,63 @@ int svo_depth_update(svo_ctx* c, const svo_camera* cam, int32_t n_kf, const svo_
     SVO_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     svo::DepthArgs a{};
-    svo_depth_seed *d_seeds = nullptr, *d_new = nullptr, *d_out = nullptr;
-    int32_t *d_outc = nullptr, *d_cseed = nullptr, *d_counts = nullptr;
-    double *d_points = nullptr, *d_cpts = nullptr, *d_kpose = nullptr, *d_cpose = nullptr;
-    const uint8_t** d_kimg = nullptr;
-    hipError_t e = hipSuccess;
-#define DALLOC(ptr, bytes) if (e == hipSuccess) e = hipMalloc(&ptr, bytes)
-    DALLOC(d_seeds, n * sizeof(svo_depth_seed));
-    DALLOC(d_new, n * sizeof(svo_depth_seed));
-    DALLOC(d_out, n * sizeof(svo_depth_seed));
-    DALLOC(d_outc, n * sizeof(int32_t));
-    DALLOC(d_cseed, n * sizeof(int32_t));
-    DALLOC(d_counts, 2 * sizeof(int32_t));
-    DALLOC(d_points, n * 3 * sizeof(double));
-    DALLOC(d_cpts, n * 3 * sizeof(double));
-    DALLOC(d_kpose, (size_t)(n_kf > 0 ? n_kf : 1) * 7 * sizeof(double));
-    DALLOC(d_cpose, 7 * sizeof(double));
-    DALLOC(d_kimg, (size_t)(n_kf > 0 ? n_kf : 1) * sizeof(void*));
-#undef DALLOC
-    if (e == hipSuccess) e = hipMemcpyAsync(d_seeds, seeds, n * sizeof(svo_depth_seed), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && n_kf > 0) e = hipMemcpyAsync(d_kpose, kf_poses, n_kf * 7 * sizeof(double), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && n_kf > 0) e = hipMemcpyAsync(d_kimg, kimg.data(), n_kf * sizeof(void*), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_cpose, cur_pose, 7 * sizeof(double), hipMemcpyHostToDevice, s);
+    // one block, same layout on both sides: inputs (seeds | keyframe poses | keyframe planes | cur pose),
+    // outputs (counts | survivors | outcomes | candidate points | candidate seeds), device-only scratch
+    // (updated seeds | points); one H2D and one D2H copy through the context's pinned staging
+    const size_t N = (size_t)n, K = (size_t)(n_kf > 0 ? n_kf : 1), SZ = sizeof(svo_depth_seed);
+    auto r8 = [](size_t v) { return (v + 7) / 8 * 8; };
+    const size_t o_seeds = 0, o_kpose = o_seeds + N * SZ, o_kimg = o_kpose + K * 56, o_cpose = o_kimg + K * 8,
+                 in_end = o_cpose + 56;
+    const size_t o_counts = in_end, o_out = o_counts + 8, o_outc = o_out + N * SZ, o_cpts = o_outc + r8(N * 4),
+                 o_cseed = o_cpts + N * 24, out_end = o_cseed + r8(N * 4);
+    const size_t o_new = out_end, o_points = o_new + N * SZ, total = o_points + N * 24;
+    void* base = nullptr;
+    void* host = nullptr;
+    std::vector<char> pageable;  // staging past kPinnedCap
+    hipError_t e = ctx_scratch(c, total, &base);
+    if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_depth_update: %s", hipGetErrorString(e));
+    if (ctx_pinned(c, out_end, &host) != hipSuccess) {
+        (void)hipGetLastError();
+        pageable.resize(out_end);
+        host = pageable.data();
+    }
+    char* hb = static_cast<char*>(host);
+    char* db = static_cast<char*>(base);
+    std::memcpy(hb + o_seeds, seeds, N * SZ);
+    if (n_kf > 0) {
+        std::memcpy(hb + o_kpose, kf_poses, (size_t)n_kf * 56);
+        std::memcpy(hb + o_kimg, kimg.data(), (size_t)n_kf * 8);
+    }
+    std::memcpy(hb + o_cpose, cur_pose, 56);
+    e = hipMemcpyAsync(db, hb, in_end, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
-        a.seeds = d_seeds; a.seeds_new = d_new; a.seeds_out = d_out; a.outcome = d_outc; a.points = d_points;
-        a.cand_points = d_cpts; a.cand_seed = d_cseed; a.counts = d_counts; a.kf_imgs = d_kimg; a.kf_poses = d_kpose;
+        a.seeds = reinterpret_cast<svo_depth_seed*>(db + o_seeds);
+        a.seeds_new = reinterpret_cast<svo_depth_seed*>(db + o_new);
+        a.seeds_out = reinterpret_cast<svo_depth_seed*>(db + o_out);
+        a.outcome = reinterpret_cast<int32_t*>(db + o_outc);
+        a.points = reinterpret_cast<double*>(db + o_points);
+        a.cand_points = reinterpret_cast<double*>(db + o_cpts);
+        a.cand_seed = reinterpret_cast<int32_t*>(db + o_cseed);
+        a.counts = reinterpret_cast<int32_t*>(db + o_counts);
+        a.kf_imgs = reinterpret_cast<const uint8_t* const*>(db + o_kimg);
+        a.kf_poses = reinterpret_cast<double*>(db + o_kpose);
         a.cur_img = cur_set->d_base + (size_t)cur_frame * cur_set->stride;
-        a.cur_pose = d_cpose;
+        a.cur_pose = reinterpret_cast<double*>(db + o_cpose);
         a.n = n; a.width = cam->width; a.height = cam->height;
         a.fx = cam->fx; a.fy = cam->fy; a.cx = cam->cx; a.cy = cam->cy;
         a.err_angle = std::atan(1.0 / (2.0 * cam->fx)) * 2.0;  // src/depth_estimator.cpp:202-206 (pixel noise 1)
         svo::launch_depth_update(a, s);
         e = hipGetLastError();
     }
-    int32_t counts[2] = {0, 0};
-    if (e == hipSuccess) e = hipMemcpyAsync(counts, d_counts, sizeof(counts), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(hb + in_end, db + in_end, out_end - in_end, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e == hipSuccess) e = hipMemcpyAsync(seeds, d_out, counts[0] * sizeof(svo_depth_seed), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && outcome) e = hipMemcpyAsync(outcome, d_outc, n * sizeof(int32_t), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(cand_points, d_cpts, counts[1] * 3 * sizeof(double), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(cand_seed, d_cseed, counts[1] * sizeof(int32_t), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    for (void* p : {(void*)d_seeds, (void*)d_new, (void*)d_out, (void*)d_outc, (void*)d_cseed, (void*)d_counts,
-                    (void*)d_points, (void*)d_cpts, (void*)d_kpose, (void*)d_cpose, (void*)d_kimg})
-        if (p) (void)hipFree(p);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_depth_update: %s", hipGetErrorString(e));
+    int32_t counts[2];
+    std::memcpy(counts, hb + o_counts, sizeof(counts));
+    std::memcpy(seeds, hb + o_out, (size_t)counts[0] * SZ);
+    if (outcome) std::memcpy(outcome, hb + o_outc, N * 4);
+    std::memcpy(cand_points, hb + o_cpts, (size_t)counts[1] * 24);
+    std::memcpy(cand_seed, hb + o_cseed, (size_t)counts[1] * 4);
     *n_out = counts[0];
     *n_cand = counts[1];
     return SVO_OK;
@@ -830,10 +880,25 @@ static int fs_detect(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_
     const uint8_t* plane = p->d_base + (size_t)frame * p->stride + p->grad_off;
     svo::launch_feature_detect(plane, p->width, p->height, threshold, d_seg, d_keys, d_n, s);
     e = hipGetLastError();
+    // the count, then the keys, through the pinned staging when it is large enough
+    void* host = nullptr;
+    const bool staged = ctx_pinned(c, (size_t)npx * 4 + 64, &host) == hipSuccess;
+    if (!staged) (void)hipGetLastError();
     int32_t cnt = 0;
-    if (e == hipSuccess) e = hipMemcpyAsync(&cnt, d_n, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    int32_t* h_n = staged ? static_cast<int32_t*>(host) : &cnt;
+    if (e == hipSuccess) e = hipMemcpyAsync(h_n, d_n, sizeof(int32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e == hipSuccess && cnt <= capacity && cnt > 0) e = hipMemcpy(keys, d_keys, (size_t)cnt * 4, hipMemcpyDeviceToHost);
+    cnt = *h_n;
+    if (e == hipSuccess && cnt <= capacity && cnt > 0) {
+        if (staged) {
+            uint32_t* hk = reinterpret_cast<uint32_t*>(static_cast<char*>(host) + 64);
+            e = hipMemcpyAsync(hk, d_keys, (size_t)cnt * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e == hipSuccess) std::memcpy(keys, hk, (size_t)cnt * 4);
+        } else {
+            e = hipMemcpy(keys, d_keys, (size_t)cnt * 4, hipMemcpyDeviceToHost);
+        }
+    }
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_detect: %s", hipGetErrorString(e));
     *n = cnt;
     return SVO_OK;
@@ -901,14 +966,28 @@ int svo_feature_select_by_value(svo_ctx* c, const svo_pyramid_set* p, int32_t fr
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_select_by_value: %s", hipGetErrorString(e));
     uint32_t* d_px = static_cast<uint32_t*>(base);
     uint8_t* d_occ = reinterpret_cast<uint8_t*>(d_px + nc);
-    std::vector<uint32_t> cell_px(nc);
-    e = hipMemcpyAsync(d_occ, occupancy, nc, hipMemcpyHostToDevice, s);
+    // pinned staging when available: [cells (4 nc) | occupancy (nc)] on both sides
+    void* host = nullptr;
+    std::vector<uint32_t> pageable;
+    uint32_t* cell_px;
+    uint8_t* h_occ;
+    if (ctx_pinned(c, (size_t)nc * 5, &host) == hipSuccess) {
+        cell_px = static_cast<uint32_t*>(host);
+        h_occ = reinterpret_cast<uint8_t*>(cell_px + nc);
+        std::memcpy(h_occ, occupancy, nc);
+    } else {
+        (void)hipGetLastError();
+        pageable.resize(nc);
+        cell_px = pageable.data();
+        h_occ = occupancy;
+    }
+    e = hipMemcpyAsync(d_occ, h_occ, nc, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         const uint8_t* plane = p->d_base + (size_t)frame * p->stride + p->grad_off;
         svo::launch_feature_cell_max(plane, W, H, cell_size, gr, gc, d_occ, threshold, d_px, s);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(cell_px.data(), d_px, (size_t)nc * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(cell_px, d_px, (size_t)nc * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_select_by_value: %s", hipGetErrorString(e));
     int32_t m = 0;
@@ -976,43 +1055,56 @@ int svo_pose_optimize(svo_ctx* c, int32_t n_frames, const int32_t* feat_off, con
                                      "(the reference dereferences a null m_point)", (long long)k);
     SVO_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    // one scratch block: offsets | poses in | poses out | err | status | bearing | point | rows | wts | flags
+    // one block, same layout on both sides: inputs (offsets | poses | bearing | point | has_point | flags)
+    // then outputs (poses | err | status | flags) then device-only scratch (rows | weights); one H2D copy
+    // of the inputs and one D2H copy of the outputs through the context's pinned staging
     const size_t F = (size_t)n_frames, N = (size_t)nf;
-    const size_t bytes = (F + 1) * 4 + 8 + F * 7 * 8 * 2 + F * 8 + F * 4 + 8 + N * 3 * 8 * 2 + N * 3 * 8 + N * 8 + N * 3 + 64;
+    auto r8 = [](size_t b) { return (b + 7) / 8 * 8; };
+    const size_t o_off = 0, o_pin = o_off + r8((F + 1) * 4), o_bear = o_pin + F * 56, o_pt = o_bear + N * 24,
+                 o_has = o_pt + N * 24, o_vin = o_has + r8(N), in_end = o_vin + r8(N);
+    const size_t o_pout = in_end, o_err = o_pout + F * 56, o_st = o_err + F * 8, o_vout = o_st + r8(F * 4),
+                 out_end = o_vout + r8(N);
+    const size_t o_rows = out_end, o_wts = o_rows + N * 24, total = o_wts + N * 8;
     void* base = nullptr;
-    hipError_t e = ctx_scratch(c, bytes, &base);
+    void* host = nullptr;
+    hipError_t e = ctx_scratch(c, total, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_pose_optimize: %s", hipGetErrorString(e));
-    char* q = static_cast<char*>(base);
-    auto take = [&](size_t b) { char* r = q; q += (b + 7) / 8 * 8; return r; };
-    int32_t* d_off = reinterpret_cast<int32_t*>(take((F + 1) * 4));
-    double* d_pin = reinterpret_cast<double*>(take(F * 7 * 8));
-    double* d_pout = reinterpret_cast<double*>(take(F * 7 * 8));
-    double* d_err = reinterpret_cast<double*>(take(F * 8));
-    int32_t* d_st = reinterpret_cast<int32_t*>(take(F * 4));
-    double* d_bear = reinterpret_cast<double*>(take(N * 3 * 8));
-    double* d_pt = reinterpret_cast<double*>(take(N * 3 * 8));
-    double* d_rows = reinterpret_cast<double*>(take(N * 3 * 8));
-    double* d_wts = reinterpret_cast<double*>(take(N * 8));
-    uint8_t* d_has = reinterpret_cast<uint8_t*>(take(N));
-    uint8_t* d_vin = reinterpret_cast<uint8_t*>(take(N));
-    uint8_t* d_vout = reinterpret_cast<uint8_t*>(take(N));
-    e = hipMemcpyAsync(d_off, feat_off, (F + 1) * 4, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_pin, poses_inout, F * 7 * 8, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && N) e = hipMemcpyAsync(d_bear, bearing, N * 3 * 8, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && N) e = hipMemcpyAsync(d_pt, point, N * 3 * 8, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && N) e = hipMemcpyAsync(d_has, has_point, N, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && N) e = hipMemcpyAsync(d_vin, vis_inout, N, hipMemcpyHostToDevice, s);
+    const bool staged = ctx_pinned(c, out_end, &host) == hipSuccess;
+    (void)hipGetLastError();
+    char* hb = static_cast<char*>(host);
+    char* db = static_cast<char*>(base);
+    struct Piece { size_t off; const void* src; size_t bytes; };
+    const Piece in[] = {{o_off, feat_off, (F + 1) * 4}, {o_pin, poses_inout, F * 56}, {o_bear, bearing, N * 24},
+                        {o_pt, point, N * 24}, {o_has, has_point, N}, {o_vin, vis_inout, N}};
+    for (const Piece& pc : in) {
+        if (!pc.bytes) continue;
+        if (staged) std::memcpy(hb + pc.off, pc.src, pc.bytes);
+        else if (e == hipSuccess) e = hipMemcpyAsync(db + pc.off, pc.src, pc.bytes, hipMemcpyHostToDevice, s);
+    }
+    if (staged && e == hipSuccess) e = hipMemcpyAsync(db, hb, in_end, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
-        svo::PoseBAArgs a{d_off, d_bear, d_pt, d_has, d_vin, d_vout, d_pin, d_pout, d_err, d_st, d_rows, d_wts, n_frames};
+        svo::PoseBAArgs a{reinterpret_cast<int32_t*>(db + o_off), reinterpret_cast<double*>(db + o_bear),
+                          reinterpret_cast<double*>(db + o_pt), reinterpret_cast<uint8_t*>(db + o_has),
+                          reinterpret_cast<uint8_t*>(db + o_vin), reinterpret_cast<uint8_t*>(db + o_vout),
+                          reinterpret_cast<double*>(db + o_pin), reinterpret_cast<double*>(db + o_pout),
+                          reinterpret_cast<double*>(db + o_err), reinterpret_cast<int32_t*>(db + o_st),
+                          reinterpret_cast<double*>(db + o_rows), reinterpret_cast<double*>(db + o_wts), n_frames};
         svo::launch_pose_ba(a, s);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(poses_inout, d_pout, F * 7 * 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(err, d_err, F * 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(status, d_st, F * 4, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && N) e = hipMemcpyAsync(vis_inout, d_vout, N, hipMemcpyDeviceToHost, s);
+    struct Out { size_t off; void* dst; size_t bytes; };
+    const Out out[] = {{o_pout, poses_inout, F * 56}, {o_err, err, F * 8}, {o_st, status, F * 4}, {o_vout, vis_inout, N}};
+    if (staged) {
+        if (e == hipSuccess) e = hipMemcpyAsync(hb + in_end, db + in_end, out_end - in_end, hipMemcpyDeviceToHost, s);
+    } else {
+        for (const Out& o : out)
+            if (o.bytes && e == hipSuccess) e = hipMemcpyAsync(o.dst, db + o.off, o.bytes, hipMemcpyDeviceToHost, s);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_pose_optimize: %s", hipGetErrorString(e));
+    if (staged)
+        for (const Out& o : out)
+            if (o.bytes) std::memcpy(o.dst, hb + o.off, o.bytes);
     return SVO_OK;
 }
 

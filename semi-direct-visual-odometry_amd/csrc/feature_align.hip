@@ -3,10 +3,10 @@
 // One 64-lane wave per candidate: the (2h+1)^2 patch (49 px at the reference's patch 7, src/map.cpp:18)
 // maps onto the wave's lanes.  Everything a lane computes is the reference's per-pixel arithmetic on the
 // level-0 GRADIENT images (float-rounded bilinear, src/algorithm.cpp:885-894); the order statistics for
-// the Tukey scale are exact ranks over the wave (the patch area is odd, so the reference's median is an
-// exact order statistic too); chi2, J^T W J and J^T W r are then summed by lane 0 in row order, the
-// reference's own order (src/optimizer.cpp:279-280), so the 3x3 system is bit-identical to the CPU
-// restatement.  Solve: Nielsen damping + Eigen-LDLT; update flow += dx (:200-205).
+// the Tukey scale are exact order statistics (a bitonic sort over the wave; the patch area is odd, so the
+// reference's median is an exact order statistic too); chi2, J^T W J and J^T W r are then summed in row
+// order, the reference's own order (src/optimizer.cpp:279-280), one accumulator per lane, so the 3x3
+// system is bit-identical to the CPU restatement.  Solve: Nielsen damping + Eigen-LDLT; update flow += dx (:200-205).
 #include "svo_internal.h"
 #include "svo_math.h"
 
@@ -31,22 +31,39 @@ __device__ __forceinline__ bool in_frame(double x, double y, double b, int W, in
     return x >= b && y >= b && x < W - b && y < H - b;
 }
 
-// k-th smallest (0-based) of v[0..m) held in LDS; every lane returns it
+// k-th smallest (0-based) of v[0..m) (m <= 128) held in LDS; every lane returns it.  Bitonic sort of
+// the m values (padded with +inf) over the wave's 64 lanes x 2 registers: element e = 64 * reg + lane;
+// partners 64 apart are in the same lane, the others one lane-xor away.
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl_xor((int)(b & 0xffffffff), m, 64), hi = __shfl_xor((int)(b >> 32), m, 64);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __device__ double wave_kth(WaveLds& L, int m, int k) {
     const int lane = threadIdx.x & 63;
-    for (int i = lane; i < m; i += 64) {
-        const double vi = L.v[i];
-        int rank = 0;
-        for (int j = 0; j < m; ++j) {
-            const double vj = L.v[j];
-            rank += (vj < vi) | ((vj == vi) & (j < i));
+    double x0 = lane < m ? L.v[lane] : __builtin_inf();
+    double x1 = lane + 64 < m ? L.v[lane + 64] : __builtin_inf();
+#pragma unroll
+    for (int size = 2; size <= 128; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride == 64) {  // size 128: ascending, partner in the other register
+                const double lo = fmin(x0, x1), hi = fmax(x0, x1);
+                x0 = lo;
+                x1 = hi;
+            } else {
+                const double p0 = shfl_xor_d(x0, stride), p1 = shfl_xor_d(x1, stride);
+                const bool lower = (lane & stride) == 0;
+                const bool asc0 = (lane & size) == 0, asc1 = ((lane + 64) & size) == 0;
+                // keep the min where (lower == ascending), else the max
+                x0 = (lower == asc0) ? fmin(x0, p0) : fmax(x0, p0);
+                x1 = (lower == asc1) ? fmin(x1, p1) : fmax(x1, p1);
+            }
         }
-        if (rank == k) L.sel = vi;
     }
-    __syncthreads();
-    const double s = L.sel;
-    __syncthreads();
-    return s;
+    const double mine = k < 64 ? x0 : x1;
+    return __shfl(mine, k & 63, 64);
 }
 
 }  // namespace
@@ -116,20 +133,32 @@ __global__ void __launch_bounds__(64 * kWavesPerBlock) feature_align_kernel(Feat
         L.w[k] = w;
     }
     __syncthreads();
-    if (active && lane == 0) {
-        double chi = 0.0, Hm[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    // chi2, J^T W J and J^T W r in row order (src/optimizer.cpp:279-280, :470-483), one accumulator per
+    // lane: lanes 0-8 H[p][q] += (J_p w) J_q, lanes 9-11 g[p] += (J_p w) r, lane 12 chi += r r w; rows
+    // with w == 0 add nothing to H and g (as the CPU restatement skips them)
+    double acc = 0.0;
+    if (active && cur_in && lane < 13) {
+        const int p = lane < 9 ? lane / 3 : lane - 9, q = lane < 9 ? lane % 3 : 0;
+        const double J2 = ref_in ? 1.0 : 0.0;
         for (int k = 0; k < A; ++k) {
-            if (!cur_in) break;
             const double r = L.r[k], w = L.w[k];
-            chi += r * r * w;
-            if (w == 0.0) continue;
-            const double J[3] = {L.jx[k], L.jy[k], ref_in ? 1.0 : 0.0};
-            for (int p = 0; p < 3; ++p) {
-                const double jw = J[p] * w;
-                for (int q = 0; q < 3; ++q) Hm[p * 3 + q] += jw * J[q];
-                g[p] += jw * r;
+            if (lane == 12) {
+                acc += r * r * w;
+            } else if (w != 0.0) {
+                const double jx = L.jx[k], jy = L.jy[k];
+                const double jw = (p == 0 ? jx : (p == 1 ? jy : J2)) * w;
+                acc += jw * (lane < 9 ? (q == 0 ? jx : (q == 1 ? jy : J2)) : r);
             }
         }
+    }
+    double sums[13];
+#pragma unroll
+    for (int t = 0; t < 13; ++t) sums[t] = __shfl(acc, t, 64);
+    if (active && lane == 0) {
+        double Hm[9], g[3];
+        for (int t = 0; t < 9; ++t) Hm[t] = sums[t];
+        for (int t = 0; t < 3; ++t) g[t] = sums[9 + t];
+        const double chi = sums[12];
         double mx = Hm[0];
         mx = fmax(mx, Hm[4]);
         mx = fmax(mx, Hm[8]);
