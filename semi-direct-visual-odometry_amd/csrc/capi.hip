@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -921,11 +922,12 @@ int svo_feature_select_ssc(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, 
     if (number_candidate < 2) return fail(SVO_ERR_ARG, "numberCandidate < 2 (SSC divides by numberCandidate - 1)");
     if (use_bucketing && (cell_size < 1 || !occupancy)) return fail(SVO_ERR_ARG, "bucketing needs cell_size and occupancy");
     const int32_t W = p->width, H = p->height;
-    std::vector<uint32_t> keys((size_t)W * H);
+    std::unique_ptr<uint32_t[]> keys(new (std::nothrow) uint32_t[(size_t)W * H]);  // not zero-filled
+    if (!keys) return fail(SVO_ERR_ARG, "out of host memory");
     int32_t n = 0;
-    if (int r = fs_detect(c, p, frame, threshold, (int32_t)keys.size(), keys.data(), &n)) return r;
+    if (int r = fs_detect(c, p, frame, threshold, W * H, keys.get(), &n)) return r;
     if (n_keypoints) *n_keypoints = n;
-    svo::feature_sort_keys(keys.data(), n);  // :53-54
+    svo::feature_sort_keys(keys.get(), n);  // :53-54
     std::vector<int32_t> xs(n), ys(n), sel;
     for (int32_t i = 0; i < n; ++i) {
         const int32_t idx = (int32_t)(keys[i] & 0xFFFFFFu);
