@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "svo_internal.h"
@@ -152,9 +153,77 @@ void launch_feature_cell_max(const uint8_t* plane, int width, int height, int ce
 }
 
 // ---------------------------------------------------------------------------------------------- host
-// std::sort with the reference's comparator (lhs.response > rhs.response, :53-54) over the keys.
+// std::sort with the reference's comparator (lhs.response > rhs.response, :53-54) over the keys, giving
+// libstdc++'s exact permutation faster.  libstdc++'s std::sort is __introsort_loop (Hoare partitions
+// around a median-of-three moved to the front, recursion on the right part, depth limit 2 floor(log2 n),
+// heap sort past it, segments of <= 16 left alone) followed by __final_insertion_sort.  Insertion sort is
+// stable, so that last pass yields the stable order by key of the partitioned array: one counting sort
+// over the 8-bit responses here.  The partition phase is restated step for step; segments at the same
+// depth are disjoint, so large ones run on their own threads without changing any step.
+namespace {
+inline bool before(uint32_t a, uint32_t b) { return (a >> 24) > (b >> 24); }
+
+inline void median_to_first(uint32_t* r, uint32_t* a, uint32_t* b, uint32_t* c) {
+    if (before(*a, *b)) {
+        if (before(*b, *c)) std::swap(*r, *b);
+        else if (before(*a, *c)) std::swap(*r, *c);
+        else std::swap(*r, *a);
+    } else if (before(*a, *c)) {
+        std::swap(*r, *a);
+    } else if (before(*b, *c)) {
+        std::swap(*r, *c);
+    } else {
+        std::swap(*r, *b);
+    }
+}
+
+inline uint32_t* partition_pivot(uint32_t* first, uint32_t* last) {
+    median_to_first(first, first + 1, first + (last - first) / 2, last - 1);
+    uint32_t* lo = first + 1;
+    uint32_t* hi = last;
+    const uint32_t pv = *first;
+    for (;;) {
+        while (before(*lo, pv)) ++lo;
+        --hi;
+        while (before(pv, *hi)) --hi;
+        if (!(lo < hi)) return lo;
+        std::swap(*lo, *hi);
+        ++lo;
+    }
+}
+
+void introsort_loop(uint32_t* first, uint32_t* last, int depth, int spawn) {
+    std::thread side;
+    while (last - first > 16) {
+        if (depth == 0) {
+            std::partial_sort(first, last, last, before);  // libstdc++ __partial_sort(first, last, last)
+            break;
+        }
+        --depth;
+        uint32_t* cut = partition_pivot(first, last);
+        if (spawn > 0 && last - cut > 8192 && !side.joinable()) {
+            side = std::thread(introsort_loop, cut, last, depth, spawn - 1);
+            --spawn;
+        } else {
+            introsort_loop(cut, last, depth, spawn > 0 ? spawn - 1 : 0);
+        }
+        last = cut;
+    }
+    if (side.joinable()) side.join();
+}
+}  // namespace
+
 void feature_sort_keys(uint32_t* keys, int32_t n) {
-    std::sort(keys, keys + n, [](uint32_t a, uint32_t b) { return (a >> 24) > (b >> 24); });
+    if (n < 2) return;
+    int lg = 0;
+    while ((2 << lg) <= n) ++lg;  // floor(log2 n)
+    introsort_loop(keys, keys + n, 2 * lg, n >= 32768 ? 3 : 0);
+    // __final_insertion_sort == stable order by response (descending)
+    uint32_t count[257] = {0};
+    for (int32_t i = 0; i < n; ++i) ++count[256 - (keys[i] >> 24)];
+    for (int v = 1; v < 257; ++v) count[v] += count[v - 1];
+    std::vector<uint32_t> tmp(keys, keys + n);
+    for (int32_t i = 0; i < n; ++i) keys[count[255 - (tmp[i] >> 24)]++] = tmp[i];
 }
 
 // SSC (src/feature_selection.cpp:166-248) over keypoints given by their (x, y) in sorted order.  Same

@@ -260,3 +260,18 @@ def test_gpu_cpp_mirror_matches_oracle(mode, tmp_path):
     got = np.array([[float(v) for v in line.split()] for line in out.splitlines()]).reshape(-1, 3)
     np.testing.assert_array_equal(got[:, :2], px)
     np.testing.assert_array_equal(got[:, 2], resp)
+
+
+def test_host_sort_is_libstdcxx_std_sort(tmp_path):
+    """svo::feature_sort_keys (a threaded restatement of libstdc++'s introsort + a counting pass for its
+    stable final insertion sort) gives std::sort's exact permutation: tests/cpp/sort_check.cpp, 112 inputs
+    (ties, sorted, reversed, all equal; sizes 0 - 150000, past the threading threshold)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    build = os.path.join(root, "semi-direct-visual-odometry_amd", "build")
+    exe = str(tmp_path / "sort_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(root, "tests", "cpp", "sort_check.cpp"),
+                    "-L" + build, "-lsvo_hip", "-Wl,-rpath," + build], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.startswith("ok"), out.stdout + out.stderr
