@@ -175,6 +175,34 @@ void FeatureSelection::setCellInGridOccupancy(const Vec2& location) {  // :276-2
 
 void FeatureSelection::resetGridOccupancy() { std::fill(m_occupancyGrid.begin(), m_occupancyGrid.end(), 0); }
 
+// ------------------------------------------------------------------ BundleAdjustment
+BundleAdjustment::BundleAdjustment(Context& ctx, std::shared_ptr<PinholeCamera> camera, int32_t level,
+                                   uint32_t numParameters)
+    : m_ctx(ctx), m_camera(std::move(camera)) {
+    if (numParameters != 6 || level != 0) throw Error(SVO_ERR_ARG, "svo: BundleAdjustment(camera, 0, 6) only");
+}
+
+double BundleAdjustment::optimizePose(std::shared_ptr<Frame>& frame) {
+    const std::size_t n = frame->numberObservation();
+    if (n == 0) return 0;  // src/bundle_adjustment.cpp:37-38
+    m_refVisibility.resize(n, 0);
+    std::vector<double> bearing(3 * n), point(3 * n, 0.0);
+    std::vector<uint8_t> has(n, 0);
+    for (std::size_t k = 0; k < n; ++k) {
+        const auto& f = frame->m_features[k];
+        for (int i = 0; i < 3; ++i) bearing[3 * k + i] = f->m_bearingVec[i];
+        if (f->m_point) {
+            has[k] = 1;
+            for (int i = 0; i < 3; ++i) point[3 * k + i] = f->m_point->m_position[i];
+        }
+    }
+    const int32_t off[2] = {0, (int32_t)n};
+    double err = 0.0;
+    check(svo_pose_optimize(m_ctx.get(), 1, off, bearing.data(), point.data(), has.data(), m_refVisibility.data(),
+                            frame->m_absPose.data(), &err, &m_status));
+    return err;
+}
+
 // ------------------------------------------------------------------ trajectory / feature dump
 namespace utils {
 void writeInFile(const Pose& refAbsPose, std::ostream& w) {

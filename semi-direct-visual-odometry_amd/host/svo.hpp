@@ -149,6 +149,23 @@ private:
     std::vector<uint8_t> m_occupancyGrid;
 };
 
+// BundleAdjustment (include/bundle_adjustment.hpp, src/bundle_adjustment.cpp:30-166): optimizePose over the
+// C ABI.  m_refVisibility is kept across calls like the reference's member (include/svo_c.h explains why
+// a fresh object returns NaN).  Several frames at once: optimizePoses.
+class BundleAdjustment {
+public:
+    BundleAdjustment(Context& ctx, std::shared_ptr<PinholeCamera> camera, int32_t level, uint32_t numParameters);
+    double optimizePose(std::shared_ptr<Frame>& frame);
+    int32_t lastStatus() const { return m_status; }
+    const std::vector<uint8_t>& refVisibility() const { return m_refVisibility; }
+
+private:
+    Context& m_ctx;
+    std::shared_ptr<PinholeCamera> m_camera;
+    std::vector<uint8_t> m_refVisibility;
+    int32_t m_status = SVO_STATUS_FAILED;
+};
+
 // Trajectory and feature-dump text, through std::ostream like the reference.
 namespace utils {
 // System::writeInFile (src/system.cpp:635-640): refAbsPose.inverse().matrix3x4() at precision 6

@@ -4,6 +4,9 @@
 //                                  FeatureSelection::gradientMagnitudeWithSSC on a raw 8-bit image (GPU);
 //                                  existing features (EX, EY) marked first; prints "x y response" per feature
 //   svo_host_check fv W H CELL THR IMAGE.raw    gradientMagnitudeByValue (bucketing)
+//   svo_host_check ba N DATA.bin   BundleAdjustment::optimizePose twice on one object (GPU); DATA.bin:
+//                                  pose[7], then per feature bearing[3] point[3] has_point (as a double);
+//                                  prints "err status qx qy qz qw tx ty tz" per call
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -51,6 +54,33 @@ int main(int argc, char** argv) {
             }
             for (const auto& f : frame->m_features)
                 std::printf("%.17g %.17g %.17g\n", f->m_pixelPosition[0], f->m_pixelPosition[1], f->m_gradientMagnitude);
+            return 0;
+        }
+        if (mode == "ba" && argc >= 4) {
+            const int n = std::atoi(argv[2]);
+            std::ifstream f(argv[3], std::ios::binary);
+            std::vector<double> d(7 + 7 * (size_t)n);
+            f.read(reinterpret_cast<char*>(d.data()), (std::streamsize)(d.size() * sizeof(double)));
+            if (!f) throw std::runtime_error("short BA data file");
+            Context ctx(0);
+            auto cam = std::make_shared<PinholeCamera>(PinholeCamera{64, 64, 300.0, 300.0, 32.0, 32.0});
+            std::vector<uint8_t> img(64 * 64, 0);
+            auto frame = std::make_shared<Frame>(ctx, cam, img.data(), 1);
+            for (int i = 0; i < 7; ++i) frame->m_absPose[i] = d[i];
+            for (int k = 0; k < n; ++k) {
+                const double* r = &d[7 + 7 * (size_t)k];
+                auto feat = std::make_shared<Feature>(frame.get(), Vec2{0.0, 0.0});
+                feat->m_bearingVec = {r[0], r[1], r[2]};
+                if (r[6] != 0.0) feat->m_point = std::make_shared<Point>(Point{{r[3], r[4], r[5]}});
+                frame->m_features.push_back(feat);
+            }
+            BundleAdjustment ba(ctx, cam, 0, 6);
+            for (int call = 0; call < 2; ++call) {
+                const double e = ba.optimizePose(frame);
+                std::printf("%.17g %d", e, ba.lastStatus());
+                for (double v : frame->m_absPose) std::printf(" %.17g", v);
+                std::printf("\n");
+            }
             return 0;
         }
         std::fprintf(stderr, "usage: svo_host_check io | fs W H CELL THR NUM BUCKET IMAGE [EX EY]... | fv W H CELL THR IMAGE\n");

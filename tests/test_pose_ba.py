@@ -206,3 +206,25 @@ def test_gpu_bundle_adjustment_object_sequence():
     assert ba.last_status == s2 and abs(e2 - o2) <= 1e-12 * o2
     np.testing.assert_allclose(canon(fr.abs_pose), canon(p2), atol=1e-12)
     np.testing.assert_array_equal(ba.ref_visibility, v2)
+
+
+@pytest.mark.gpu
+def test_gpu_cpp_mirror_bundle_adjustment(tmp_path):
+    """host/svo.hpp BundleAdjustment (libsvo_host.so via build/svo_host_check ba): two optimizePose calls on
+    one object against the oracle's sequence."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "semi-direct-visual-odometry_amd", "build", "svo_host_check")
+    b, P, has, init = scene(21, 200)
+    data = np.concatenate([init, np.concatenate([b, P, has[:, None].astype(np.float64)], axis=1).ravel()])
+    path = tmp_path / "ba.bin"
+    path.write_bytes(data.astype(np.float64).tobytes())
+    out = subprocess.run([exe, "ba", str(len(has)), str(path)], capture_output=True, text=True, timeout=60, check=True)
+    lines = [[float(v) for v in line.split()] for line in out.stdout.splitlines()]
+    p1, e1, s1, v1 = O.optimize_pose(b, P, has, [], init)
+    p2, e2, s2, _ = O.optimize_pose(b, P, has, v1, p1)
+    assert np.isnan(lines[0][0]) and int(lines[0][1]) == s1
+    np.testing.assert_allclose(canon(lines[0][2:]), canon(p1), atol=1e-12)
+    assert abs(lines[1][0] - e2) <= 1e-12 * e2 and int(lines[1][1]) == s2
+    np.testing.assert_allclose(canon(lines[1][2:]), canon(p2), atol=1e-12)
