@@ -203,6 +203,56 @@ double BundleAdjustment::optimizePose(std::shared_ptr<Frame>& frame) {
     return err;
 }
 
+// ------------------------------------------------------------------ DepthEstimator
+void DepthEstimator::addKeyframe(const std::shared_ptr<Frame>& frame, double depthMean, double depthMin) {
+    const int32_t kf = (int32_t)m_keyframes.size();
+    m_keyframes.push_back(frame);
+    for (const auto& f : frame->m_features) {
+        if (f->m_point) continue;  // initializeFilters: features without a point only
+        svo_depth_seed sd{};
+        check(svo_depth_seed_init(depthMean, depthMin, &sd));  // MixedGaussianFilter (src/mixed_gaussian_filter.cpp:7-24)
+        sd.px[0] = f->m_pixelPosition[0];
+        sd.px[1] = f->m_pixelPosition[1];
+        for (int i = 0; i < 3; ++i) sd.bearing[i] = f->m_bearingVec[i];
+        sd.kf = kf;
+        m_seeds.push_back(sd);
+        m_features.push_back(f);
+    }
+}
+
+std::vector<std::pair<std::shared_ptr<Feature>, std::shared_ptr<Point>>> DepthEstimator::updateFilters(
+    const std::shared_ptr<Frame>& frame) {
+    std::vector<std::pair<std::shared_ptr<Feature>, std::shared_ptr<Point>>> out;
+    const int32_t n = (int32_t)m_seeds.size();
+    if (n == 0) return out;
+    const int32_t nk = (int32_t)m_keyframes.size();
+    std::vector<const svo_pyramid_set*> sets(nk);
+    std::vector<int32_t> frames(nk, 0);
+    std::vector<double> poses(7 * (size_t)nk);
+    for (int32_t k = 0; k < nk; ++k) {
+        sets[k] = m_keyframes[k]->m_imagePyramid.set();
+        for (int i = 0; i < 7; ++i) poses[7 * k + i] = m_keyframes[k]->m_absPose[i];
+    }
+    std::vector<int32_t> outcome(n), cand_seed(n);
+    std::vector<double> cand_points(3 * (size_t)n);
+    int32_t n_out = 0, n_cand = 0;
+    const svo_camera cam = frame->m_camera->c();
+    std::vector<svo_depth_seed> seeds = m_seeds;
+    check(svo_depth_update(m_ctx.get(), &cam, nk, sets.data(), frames.data(), poses.data(), frame->m_imagePyramid.set(),
+                           0, frame->m_absPose.data(), n, seeds.data(), &n_out, outcome.data(), cand_points.data(),
+                           cand_seed.data(), &n_cand));
+    for (int32_t j = 0; j < n_cand; ++j)
+        out.emplace_back(m_features[cand_seed[j]],
+                         std::make_shared<Point>(Point{{cand_points[3 * j], cand_points[3 * j + 1], cand_points[3 * j + 2]}}));
+    std::vector<std::shared_ptr<Feature>> keep;  // survivors, order kept (remove_if, :300-308)
+    for (int32_t i = 0; i < n; ++i)
+        if (outcome[i] == SVO_DEPTH_NO_MATCH || outcome[i] == SVO_DEPTH_UPDATED) keep.push_back(m_features[i]);
+    m_features.swap(keep);
+    seeds.resize(n_out);
+    m_seeds.swap(seeds);
+    return out;
+}
+
 // ------------------------------------------------------------------ trajectory / feature dump
 namespace utils {
 void writeInFile(const Pose& refAbsPose, std::ostream& w) {

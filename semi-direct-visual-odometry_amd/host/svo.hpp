@@ -13,6 +13,7 @@
 #include <memory>
 #include <ostream>
 #include <stdexcept>
+#include <utility>
 #include <vector>
 
 #include "svo_c.h"
@@ -164,6 +165,25 @@ private:
     std::shared_ptr<PinholeCamera> m_camera;
     std::vector<uint8_t> m_refVisibility;
     int32_t m_status = SVO_STATUS_FAILED;
+};
+
+// DepthEstimator (include/depth_estimator.hpp, src/depth_estimator.cpp:175-309) without its worker thread:
+// addKeyframe = initializeFilters for the keyframe's features without a point; updateFilters = one
+// svo_depth_update over every seed.  Converged seeds come back as (feature, point) candidates in the
+// reference's order (Map::addNewCandidate, src/map.cpp:586-593).
+class DepthEstimator {
+public:
+    explicit DepthEstimator(Context& ctx) : m_ctx(ctx) {}
+    void addKeyframe(const std::shared_ptr<Frame>& frame, double depthMean, double depthMin);
+    std::vector<std::pair<std::shared_ptr<Feature>, std::shared_ptr<Point>>> updateFilters(const std::shared_ptr<Frame>& frame);
+    std::size_t numberFilters() const { return m_seeds.size(); }
+    const std::vector<svo_depth_seed>& seeds() const { return m_seeds; }
+
+private:
+    Context& m_ctx;
+    std::vector<std::shared_ptr<Frame>> m_keyframes;  // svo_depth_seed::kf indexes this list
+    std::vector<std::shared_ptr<Feature>> m_features; // the feature behind every seed
+    std::vector<svo_depth_seed> m_seeds;
 };
 
 // Trajectory and feature-dump text, through std::ostream like the reference.

@@ -7,6 +7,10 @@
 //   svo_host_check ba N DATA.bin   BundleAdjustment::optimizePose twice on one object (GPU); DATA.bin:
 //                                  pose[7], then per feature bearing[3] point[3] has_point (as a double);
 //                                  prints "err status qx qy qz qw tx ty tz" per call
+//   svo_host_check depth DATA.bin KF.raw CUR.raw   DepthEstimator addKeyframe + updateFilters (GPU);
+//                                  DATA.bin: fx fy cx cy W H, kf pose[7], cur pose[7], depth_mean, depth_min,
+//                                  n, then n x (px[2] bearing[3]) as doubles; prints "filters M", then one
+//                                  "cand X Y Z" line per candidate
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -81,6 +85,37 @@ int main(int argc, char** argv) {
                 for (double v : frame->m_absPose) std::printf(" %.17g", v);
                 std::printf("\n");
             }
+            return 0;
+        }
+        if (mode == "depth" && argc >= 5) {
+            std::ifstream f(argv[2], std::ios::binary);
+            std::vector<double> hdr(6 + 7 + 7 + 3);
+            f.read(reinterpret_cast<char*>(hdr.data()), (std::streamsize)(hdr.size() * sizeof(double)));
+            const int w = (int)hdr[4], h = (int)hdr[5], n = (int)hdr[22];
+            std::vector<double> d(5 * (size_t)n);
+            f.read(reinterpret_cast<char*>(d.data()), (std::streamsize)(d.size() * sizeof(double)));
+            if (!f) throw std::runtime_error("short depth data file");
+            const std::vector<uint8_t> kimg = read_raw(argv[3], (size_t)w * h), cimg = read_raw(argv[4], (size_t)w * h);
+            Context ctx(0);
+            auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, hdr[0], hdr[1], hdr[2], hdr[3]});
+            auto kf = std::make_shared<Frame>(ctx, cam, kimg.data(), 1);
+            auto cur = std::make_shared<Frame>(ctx, cam, cimg.data(), 1);
+            for (int i = 0; i < 7; ++i) {
+                kf->m_absPose[i] = hdr[6 + i];
+                cur->m_absPose[i] = hdr[13 + i];
+            }
+            for (int k = 0; k < n; ++k) {
+                const double* r = &d[5 * (size_t)k];
+                auto feat = std::make_shared<Feature>(kf.get(), Vec2{r[0], r[1]});
+                feat->m_bearingVec = {r[2], r[3], r[4]};
+                kf->m_features.push_back(feat);
+            }
+            DepthEstimator de(ctx);
+            de.addKeyframe(kf, hdr[20], hdr[21]);
+            const auto cands = de.updateFilters(cur);
+            std::printf("filters %zu\n", de.numberFilters());
+            for (const auto& c : cands)
+                std::printf("cand %.17g %.17g %.17g\n", c.second->m_position[0], c.second->m_position[1], c.second->m_position[2]);
             return 0;
         }
         std::fprintf(stderr, "usage: svo_host_check io | fs W H CELL THR NUM BUCKET IMAGE [EX EY]... | fv W H CELL THR IMAGE\n");

@@ -164,3 +164,31 @@ def test_gpu_depth_estimator_class_surface():
     new = de.update_filters(cur)
     assert len(new) == len(p.px) and de.number_filters() == 0
     assert all(abs(pt.position[2] - 10.0) < 0.3 for _, pt in new)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("problem", ["config5", "plane"])
+def test_gpu_cpp_mirror_depth_estimator(problem, tmp_path):
+    """host/svo.hpp DepthEstimator (libsvo_host.so via build/svo_host_check depth): addKeyframe +
+    updateFilters against the oracle: surviving filter count, candidate points in the reference's order
+    (1e-12 relative, the device acos / sin / exp)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "semi-direct-visual-odometry_amd", "build", "svo_host_check")
+    p = synth.make_depth_problem(n_seeds=2000) if problem == "config5" else synth.make_shifted_plane()
+    c = p.camera
+    hdr = [c["fx"], c["fy"], c["cx"], c["cy"], c["width"], c["height"], *p.kf_pose, *p.cur_pose, p.depth_mean,
+           p.depth_min, len(p.px)]
+    data = np.concatenate([np.array(hdr, np.float64), np.concatenate([p.px, p.bearing], axis=1).ravel()])
+    (tmp_path / "d.bin").write_bytes(data.astype(np.float64).tobytes())
+    (tmp_path / "kf.raw").write_bytes(np.ascontiguousarray(p.kf_img).tobytes())
+    (tmp_path / "cur.raw").write_bytes(np.ascontiguousarray(p.cur_img).tobytes())
+    out = subprocess.run([exe, "depth", str(tmp_path / "d.bin"), str(tmp_path / "kf.raw"), str(tmp_path / "cur.raw")],
+                         capture_output=True, text=True, timeout=60, check=True).stdout.splitlines()
+    seeds = O.make_seeds(p.px, p.bearing, p.depth_mean, p.depth_min)
+    surv, outc, pts, cs = O.depth_update(c, [p.kf_img], p.kf_pose[None], p.cur_img, p.cur_pose, seeds)
+    assert out[0] == f"filters {len(surv)}"
+    got = np.array([[float(v) for v in line.split()[1:]] for line in out[1:]]).reshape(-1, 3)
+    assert got.shape == pts.shape
+    np.testing.assert_allclose(got, pts, rtol=1e-12, atol=1e-12)
