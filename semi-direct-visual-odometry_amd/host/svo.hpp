@@ -77,8 +77,15 @@ private:
 };
 
 struct Frame;
-struct Point {
+struct Feature;
+struct Point {  // include/point.hpp:14-40 (the members the map's reprojection reads and writes)
+    enum class PointType : uint32_t { GOOD = 0, DELETED = 1, CANDIDATE = 2, UNKNOWN = 3 };
     Vec3 m_position;
+    PointType m_type = PointType::UNKNOWN;
+    uint64_t m_lastProjectedKFId = ~(uint64_t)0;  // m_lastProjectedKFId(-1)
+    uint32_t m_succeededProjection = 0;
+    uint32_t m_failedProjection = 0;
+    std::vector<std::weak_ptr<Feature>> m_features;  // observing features (weak: Frame owns them)
 };
 struct Feature {  // include/feature.hpp:14
     enum class FeatureType : uint32_t { EDGE = 0, CORNER = 1 };  // include/feature.hpp:19-23
@@ -99,6 +106,7 @@ struct Frame {  // include/frame.hpp:70-208 (the members the alignment path read
     ImagePyramid m_imagePyramid;
     std::vector<std::shared_ptr<Feature>> m_features;
     std::shared_ptr<Frame> m_lastKeyframe;
+    uint64_t m_id;  // Frame::m_frameCounter (src/frame.cpp:6-27)
     std::size_t numberObservation() const { return m_features.size(); }
 };
 
@@ -184,6 +192,35 @@ private:
     std::vector<std::shared_ptr<Frame>> m_keyframes;  // svo_depth_seed::kf indexes this list
     std::vector<std::shared_ptr<Feature>> m_features; // the feature behind every seed
     std::vector<svo_depth_seed> m_seeds;
+};
+
+// Map (include/map.hpp, src/map.cpp:15-634): the reprojection half — reprojectMap (:260-570) as one
+// host plan (svo_map_reproject_plan) plus one batched FeatureAlignment(7) launch, addNewCandidate
+// (:586-593) and addCandidateToFrame (:595-627) with one launch for every candidate in a free cell.  The
+// cell order is a seeded permutation (the reference shuffles with an unseeded std::random_device) or the
+// caller's.
+class Map {
+public:
+    Map(Context& ctx, std::shared_ptr<PinholeCamera> camera, int32_t cellSize, uint64_t seed = 0);
+    void setCellOrder(const std::vector<int32_t>& order) { m_cellOrders = order; }
+    void reprojectMap(const std::shared_ptr<Frame>& refFrame, std::shared_ptr<Frame>& curFrame,
+                      std::vector<std::pair<std::shared_ptr<Frame>, int32_t>>& overlapKeyFrames);
+    void addNewCandidate(const std::shared_ptr<Feature>& feature, const std::shared_ptr<Point>& point);
+    void addCandidateToFrame(std::shared_ptr<Frame>& frame);
+    uint32_t m_matches = 0, m_trials = 0;
+    std::vector<int32_t> m_cellOrders;
+    std::vector<uint8_t> m_cellVisited;  // never cleared, as in the reference
+    struct Candidate {
+        std::shared_ptr<Feature> feature;
+        std::shared_ptr<Point> point;
+        bool matched;
+    };
+    std::vector<Candidate> m_candidates;
+
+private:
+    Context& m_ctx;
+    std::shared_ptr<PinholeCamera> m_camera;
+    int32_t m_cellSize, m_gridCols, m_gridRows;
 };
 
 // Trajectory and feature-dump text, through std::ostream like the reference.

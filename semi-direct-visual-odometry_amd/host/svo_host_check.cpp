@@ -11,6 +11,11 @@
 //                                  DATA.bin: fx fy cx cy W H, kf pose[7], cur pose[7], depth_mean, depth_min,
 //                                  n, then n x (px[2] bearing[3]) as doubles; prints "filters M", then one
 //                                  "cand X Y Z" line per candidate
+//   svo_host_check map DATA.bin REF.raw KF.raw CUR.raw   Map::reprojectMap + addCandidateToFrame (GPU);
+//                                  DATA.bin (doubles): fx fy cx cy W H cell, ref/kf/cur pose[7], n_ref n_kf
+//                                  n_points n_cand n_cells, feat_px[2n], feat_point[n], point_pos[3p],
+//                                  point_type[p], point_succ[p], cand_feat[c], cand_pos[3c], cell_order;
+//                                  prints "counts matches trials", then "px X Y" per new cur feature
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -116,6 +121,61 @@ int main(int argc, char** argv) {
             std::printf("filters %zu\n", de.numberFilters());
             for (const auto& c : cands)
                 std::printf("cand %.17g %.17g %.17g\n", c.second->m_position[0], c.second->m_position[1], c.second->m_position[2]);
+            return 0;
+        }
+        if (mode == "map" && argc >= 6) {
+            std::ifstream f(argv[2], std::ios::binary);
+            f.seekg(0, std::ios::end);
+            const size_t bytes = (size_t)f.tellg();
+            f.seekg(0);
+            std::vector<double> v(bytes / sizeof(double));
+            f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)bytes);
+            size_t q = 0;
+            auto take = [&]() { return v.at(q++); };
+            const double fx = take(), fy = take(), cx = take(), cy = take();
+            const int w = (int)take(), h = (int)take(), cell = (int)take();
+            Pose poses[3];
+            for (auto& p : poses)
+                for (double& x : p) x = take();
+            const int nref = (int)take(), nkf = (int)take(), npt = (int)take(), nc = (int)take(), ncells = (int)take();
+            const int nf = nref + nkf;
+            const std::vector<uint8_t> rimg = read_raw(argv[3], (size_t)w * h), kimg = read_raw(argv[4], (size_t)w * h),
+                                       cimg = read_raw(argv[5], (size_t)w * h);
+            Context ctx(0);
+            auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, fx, fy, cx, cy});
+            auto kf = std::make_shared<Frame>(ctx, cam, kimg.data(), 1);
+            auto ref = std::make_shared<Frame>(ctx, cam, rimg.data(), 1, kf);
+            auto cur = std::make_shared<Frame>(ctx, cam, cimg.data(), 1, kf);
+            ref->m_absPose = poses[0];
+            kf->m_absPose = poses[1];
+            cur->m_absPose = poses[2];
+            std::vector<Vec2> px(nf);
+            for (auto& p : px) p = {take(), take()};
+            std::vector<int> fpt(nf);
+            for (int& i : fpt) i = (int)take();
+            std::vector<std::shared_ptr<Point>> pts(npt);
+            for (auto& p : pts) p = std::make_shared<Point>(Point{{take(), take(), take()}});
+            for (auto& p : pts) p->m_type = (Point::PointType)(uint32_t)take();
+            for (auto& p : pts) p->m_succeededProjection = (uint32_t)take();
+            std::vector<std::shared_ptr<Feature>> feats(nf);
+            for (int i = 0; i < nf; ++i) {
+                Frame* fr = i < nref ? ref.get() : kf.get();
+                feats[i] = std::make_shared<Feature>(fr, px[i]);
+                if (fpt[i] >= 0) feats[i]->m_point = pts[fpt[i]];
+                (i < nref ? ref : kf)->m_features.push_back(feats[i]);
+            }
+            Map map(ctx, cam, cell);
+            std::vector<int> cf(nc);
+            for (int& i : cf) i = (int)take();
+            for (int i = 0; i < nc; ++i) map.addNewCandidate(feats[cf[i]], std::make_shared<Point>(Point{{take(), take(), take()}}));
+            std::vector<int32_t> order(ncells);
+            for (int32_t& o : order) o = (int32_t)take();
+            map.setCellOrder(order);
+            std::vector<std::pair<std::shared_ptr<Frame>, int32_t>> overlap;
+            map.reprojectMap(ref, cur, overlap);
+            map.addCandidateToFrame(cur);
+            std::printf("counts %u %u\n", map.m_matches, map.m_trials);
+            for (const auto& ft : cur->m_features) std::printf("px %.17g %.17g\n", ft->m_pixelPosition[0], ft->m_pixelPosition[1]);
             return 0;
         }
         std::fprintf(stderr, "usage: svo_host_check io | fs W H CELL THR NUM BUCKET IMAGE [EX EY]... | fv W H CELL THR IMAGE\n");

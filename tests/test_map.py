@@ -151,3 +151,42 @@ def test_gpu_map_needs_last_keyframe():
     ref.last_keyframe = None
     with pytest.raises(ValueError):
         m.reproject_map(ref, cur, [])
+
+
+@pytest.mark.gpu
+def test_gpu_cpp_mirror_map(tmp_path):
+    """host/svo.hpp Map (libsvo_host.so via build/svo_host_check map): reprojectMap + addCandidateToFrame on a
+    config-2 map against the sequential oracle: the same new features, bit-exact, in the same order."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "semi-direct-visual-odometry_amd", "build", "svo_host_check")
+    mp = synth.make_map_problem()
+    c = mp.camera
+    W, H = c["width"], c["height"]
+    ncells = math.ceil(W / mp.cell_size) * math.ceil(H / mp.cell_size)
+    order = np.random.default_rng(5).permutation(ncells).astype(np.int32)
+    parts = [[c["fx"], c["fy"], c["cx"], c["cy"], W, H, mp.cell_size], mp.ref_pose, mp.kf_pose, mp.cur_pose,
+             [mp.n_ref, mp.n_kf, len(mp.point_pos), len(mp.cand_feat), ncells], mp.feat_px.ravel(), mp.feat_point,
+             mp.point_pos.ravel(), mp.point_type, mp.point_succ, mp.cand_feat, mp.cand_pos.ravel(), order]
+    data = np.concatenate([np.asarray(x, np.float64).ravel() for x in parts])
+    (tmp_path / "m.bin").write_bytes(data.tobytes())
+    for name, img in (("ref", mp.ref_img), ("kf", mp.kf_img), ("cur", mp.cur_img)):
+        (tmp_path / f"{name}.raw").write_bytes(np.ascontiguousarray(img).tobytes())
+    out = subprocess.run([exe, "map", str(tmp_path / "m.bin"), str(tmp_path / "ref.raw"), str(tmp_path / "kf.raw"),
+                          str(tmp_path / "cur.raw")], capture_output=True, text=True, timeout=60, check=True)
+    lines = out.stdout.splitlines()
+    got = np.array([[float(v) for v in l.split()[1:]] for l in lines[1:]]).reshape(-1, 2)
+    grad = {k: O.unpack_levels(O.build_pyramid(img, 1)[1], W, H, 1)[0]
+            for k, img in (("ref", mp.ref_img), ("kf", mp.kf_img), ("cur", mp.cur_img))}
+    ptype, psucc = mp.point_type.copy(), mp.point_succ.copy()
+    plast = np.full(len(mp.point_pos), np.uint64(2 ** 64 - 1), np.uint64)
+    visited = np.zeros(ncells, np.uint8)
+    rep = O.reproject_map(mp.camera, mp.cell_size, order, mp.cur_pose, 7, grad["cur"], [grad["ref"], grad["kf"]],
+                          np.array([0, mp.n_ref, mp.n_ref + mp.n_kf], np.int32), mp.feat_px, mp.feat_point,
+                          mp.point_pos, ptype, psucc, plast, visited)
+    cm, cpx = O.add_candidates(mp.camera, mp.cell_size, visited, mp.cur_pose, grad["cur"], [grad["kf"]] * len(mp.cand_feat),
+                               mp.feat_px[mp.cand_feat], mp.cand_pos)
+    expect = np.concatenate([rep[1], cpx[cm]])
+    assert lines[0] == f"counts {rep[4]} {rep[5]}"
+    np.testing.assert_array_equal(got, expect)
