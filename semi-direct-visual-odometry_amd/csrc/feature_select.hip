@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -159,7 +160,7 @@ void launch_feature_cell_max(const uint8_t* plane, int width, int height, int ce
 // heap sort past it, segments of <= 16 left alone) followed by __final_insertion_sort.  Insertion sort is
 // stable, so that last pass yields the stable order by key of the partitioned array: one counting sort
 // over the 8-bit responses here.  The partition phase is restated step for step; segments at the same
-// depth are disjoint, so large ones run on their own threads without changing any step.
+// depth are disjoint, so large ones run on their own threads (up to 7) without changing any step.
 namespace {
 inline bool before(uint32_t a, uint32_t b) { return (a >> 24) > (b >> 24); }
 
@@ -192,8 +193,11 @@ inline uint32_t* partition_pivot(uint32_t* first, uint32_t* last) {
     }
 }
 
-void introsort_loop(uint32_t* first, uint32_t* last, int depth, int spawn) {
-    std::thread side;
+// segments above kSpawnMin take a thread of their own while the budget lasts
+constexpr ptrdiff_t kSpawnMin = 8192;
+
+void introsort_loop(uint32_t* first, uint32_t* last, int depth, std::atomic<int>* budget) {
+    std::vector<std::thread> sides;
     while (last - first > 16) {
         if (depth == 0) {
             std::partial_sort(first, last, last, before);  // libstdc++ __partial_sort(first, last, last)
@@ -201,15 +205,15 @@ void introsort_loop(uint32_t* first, uint32_t* last, int depth, int spawn) {
         }
         --depth;
         uint32_t* cut = partition_pivot(first, last);
-        if (spawn > 0 && last - cut > 8192 && !side.joinable()) {
-            side = std::thread(introsort_loop, cut, last, depth, spawn - 1);
-            --spawn;
+        if (budget && last - cut > kSpawnMin && budget->fetch_sub(1) > 0) {
+            sides.emplace_back(introsort_loop, cut, last, depth, budget);
         } else {
-            introsort_loop(cut, last, depth, spawn > 0 ? spawn - 1 : 0);
+            if (budget && last - cut > kSpawnMin) budget->fetch_add(1);
+            introsort_loop(cut, last, depth, budget);
         }
         last = cut;
     }
-    if (side.joinable()) side.join();
+    for (std::thread& t : sides) t.join();
 }
 }  // namespace
 
@@ -217,7 +221,8 @@ void feature_sort_keys(uint32_t* keys, int32_t n) {
     if (n < 2) return;
     int lg = 0;
     while ((2 << lg) <= n) ++lg;  // floor(log2 n)
-    introsort_loop(keys, keys + n, 2 * lg, n >= 32768 ? 3 : 0);
+    std::atomic<int> budget(7);  // extra threads
+    introsort_loop(keys, keys + n, 2 * lg, n >= 32768 ? &budget : nullptr);
     // __final_insertion_sort == stable order by response (descending)
     uint32_t count[257] = {0};
     for (int32_t i = 0; i < n; ++i) ++count[256 - (keys[i] >> 24)];
