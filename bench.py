@@ -298,13 +298,29 @@ def secondary(args, ctx, scene, cam, camera, reps=20):
         for fr in (ref, kf, cur):
             fr.image_pyramid.clear()
     del graphs
+    # the same call through the C++ mirror (host/svo.hpp Map via build/svo_host_check map ... REPS): what a
+    # C++ caller of the C ABI pays per frame; reported only when its output is the oracle's, bit for bit
+    cpp_ms = None
+    exe = os.path.join(ROOT, "semi-direct-visual-odometry_amd", "build", "svo_host_check")
+    if os.path.exists(exe):
+        import subprocess
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            paths = synth.write_map_problem(mp, td, m0.cell_orders)
+            r = subprocess.run([exe, "map", *paths, str(reps)], capture_output=True, text=True, timeout=120)
+            lines = r.stdout.splitlines() if r.returncode == 0 else []
+            cpx_cpp = np.array([[float(v) for v in ln.split()[1:]] for ln in lines if ln.startswith("px ")])
+            if lines and lines[-1].startswith("ms ") and np.array_equal(cpx_cpp.reshape(-1, 2), expect):
+                cpp_ms = float(lines[-1].split()[1])
     res["map_reproject"] = {
         "map_points": len(mp.point_pos), "candidates": len(mp.cand_feat), "matches": int(rep[4]),
         "new_features": int(len(expect)), "gpu_ms_per_call": round(g * 1e3, 4),
-        "native_ms_per_call": round(native * 1e3, 4), "cpu_ms_1_thread": round(c * 1e3, 3),
+        "native_ms_per_call": round(native * 1e3, 4),
+        "cpp_mirror_ms_per_call": None if cpp_ms is None else round(cpp_ms, 4), "cpu_ms_1_thread": round(c * 1e3, 3),
         "bitexact_vs_oracle": bool(np.array_equal(news[0], expect)),
         "note": "gpu: end to end per frame through the Python mirror (object bookkeeping included); native: the "
-                "time inside the C ABI calls (host plan, projection, two batched FeatureAlignment launches)"}
+                "time inside the C ABI calls (host plan, projection, two batched FeatureAlignment launches); "
+                "cpp_mirror: end to end through the C++ Map (null unless its output equals the oracle's)"}
     # FeatureSelection on a KITTI-shaped keyframe (threshold 50, 200 candidates,
     # bucketing in 30-px cells: src/system.cpp:253, config/config.json).  gpu = the whole call (device
     # detection + D2H of the keys + host std::sort / SSC); detect_call = svo_feature_detect alone (2 kernels +

@@ -15,7 +15,10 @@
 //                                  DATA.bin (doubles): fx fy cx cy W H cell, ref/kf/cur pose[7], n_ref n_kf
 //                                  n_points n_cand n_cells, feat_px[2n], feat_point[n], point_pos[3p],
 //                                  point_type[p], point_succ[p], cand_feat[c], cand_pos[3c], cell_order;
-//                                  prints "counts matches trials", then "px X Y" per new cur feature
+//                                  prints "counts matches trials", then "px X Y" per new cur feature;
+//                                  an optional REPS argument also times REPS more runs on fresh object
+//                                  graphs ("ms T": reprojectMap + addCandidateToFrame, average)
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
@@ -139,43 +142,64 @@ int main(int argc, char** argv) {
                 for (double& x : p) x = take();
             const int nref = (int)take(), nkf = (int)take(), npt = (int)take(), nc = (int)take(), ncells = (int)take();
             const int nf = nref + nkf;
-            const std::vector<uint8_t> rimg = read_raw(argv[3], (size_t)w * h), kimg = read_raw(argv[4], (size_t)w * h),
-                                       cimg = read_raw(argv[5], (size_t)w * h);
-            Context ctx(0);
-            auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, fx, fy, cx, cy});
-            auto kf = std::make_shared<Frame>(ctx, cam, kimg.data(), 1);
-            auto ref = std::make_shared<Frame>(ctx, cam, rimg.data(), 1, kf);
-            auto cur = std::make_shared<Frame>(ctx, cam, cimg.data(), 1, kf);
-            ref->m_absPose = poses[0];
-            kf->m_absPose = poses[1];
-            cur->m_absPose = poses[2];
             std::vector<Vec2> px(nf);
             for (auto& p : px) p = {take(), take()};
             std::vector<int> fpt(nf);
             for (int& i : fpt) i = (int)take();
-            std::vector<std::shared_ptr<Point>> pts(npt);
-            for (auto& p : pts) p = std::make_shared<Point>(Point{{take(), take(), take()}});
-            for (auto& p : pts) p->m_type = (Point::PointType)(uint32_t)take();
-            for (auto& p : pts) p->m_succeededProjection = (uint32_t)take();
-            std::vector<std::shared_ptr<Feature>> feats(nf);
-            for (int i = 0; i < nf; ++i) {
-                Frame* fr = i < nref ? ref.get() : kf.get();
-                feats[i] = std::make_shared<Feature>(fr, px[i]);
-                if (fpt[i] >= 0) feats[i]->m_point = pts[fpt[i]];
-                (i < nref ? ref : kf)->m_features.push_back(feats[i]);
-            }
-            Map map(ctx, cam, cell);
+            std::vector<Vec3> ppos(npt);
+            for (auto& p : ppos) p = {take(), take(), take()};
+            std::vector<uint32_t> ptype(npt), psucc(npt);
+            for (auto& t : ptype) t = (uint32_t)take();
+            for (auto& t : psucc) t = (uint32_t)take();
             std::vector<int> cf(nc);
             for (int& i : cf) i = (int)take();
-            for (int i = 0; i < nc; ++i) map.addNewCandidate(feats[cf[i]], std::make_shared<Point>(Point{{take(), take(), take()}}));
+            std::vector<Vec3> cpos(nc);
+            for (auto& p : cpos) p = {take(), take(), take()};
             std::vector<int32_t> order(ncells);
             for (int32_t& o : order) o = (int32_t)take();
-            map.setCellOrder(order);
-            std::vector<std::pair<std::shared_ptr<Frame>, int32_t>> overlap;
-            map.reprojectMap(ref, cur, overlap);
-            map.addCandidateToFrame(cur);
-            std::printf("counts %u %u\n", map.m_matches, map.m_trials);
-            for (const auto& ft : cur->m_features) std::printf("px %.17g %.17g\n", ft->m_pixelPosition[0], ft->m_pixelPosition[1]);
+            const std::vector<uint8_t> rimg = read_raw(argv[3], (size_t)w * h), kimg = read_raw(argv[4], (size_t)w * h),
+                                       cimg = read_raw(argv[5], (size_t)w * h);
+            const int reps = argc >= 7 ? std::atoi(argv[6]) : 0;  // > 0: time reprojectMap + addCandidateToFrame
+            Context ctx(0);
+            auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, fx, fy, cx, cy});
+            double total_ms = 0.0;
+            for (int rep = 0; rep <= reps; ++rep) {
+                // a fresh object graph per run (the calls mutate the map, the points and the cur frame)
+                auto kf = std::make_shared<Frame>(ctx, cam, kimg.data(), 1);
+                auto ref = std::make_shared<Frame>(ctx, cam, rimg.data(), 1, kf);
+                auto cur = std::make_shared<Frame>(ctx, cam, cimg.data(), 1, kf);
+                ref->m_absPose = poses[0];
+                kf->m_absPose = poses[1];
+                cur->m_absPose = poses[2];
+                std::vector<std::shared_ptr<Point>> pts(npt);
+                for (int i = 0; i < npt; ++i) {
+                    pts[i] = std::make_shared<Point>(Point{ppos[i]});
+                    pts[i]->m_type = (Point::PointType)ptype[i];
+                    pts[i]->m_succeededProjection = psucc[i];
+                }
+                std::vector<std::shared_ptr<Feature>> feats(nf);
+                for (int i = 0; i < nf; ++i) {
+                    feats[i] = std::make_shared<Feature>(i < nref ? ref.get() : kf.get(), px[i]);
+                    if (fpt[i] >= 0) feats[i]->m_point = pts[fpt[i]];
+                    (i < nref ? ref : kf)->m_features.push_back(feats[i]);
+                }
+                Map map(ctx, cam, cell);
+                for (int i = 0; i < nc; ++i) map.addNewCandidate(feats[cf[i]], std::make_shared<Point>(Point{cpos[i]}));
+                map.setCellOrder(order);
+                std::vector<std::pair<std::shared_ptr<Frame>, int32_t>> overlap;
+                (void)svo_ctx_synchronize(ctx.get());
+                const auto t0 = std::chrono::steady_clock::now();
+                map.reprojectMap(ref, cur, overlap);
+                map.addCandidateToFrame(cur);
+                const auto t1 = std::chrono::steady_clock::now();
+                if (rep > 0) total_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+                if (rep == 0) {
+                    std::printf("counts %u %u\n", map.m_matches, map.m_trials);
+                    for (const auto& ft : cur->m_features)
+                        std::printf("px %.17g %.17g\n", ft->m_pixelPosition[0], ft->m_pixelPosition[1]);
+                }
+            }
+            if (reps > 0) std::printf("ms %.6f\n", total_ms / reps);
             return 0;
         }
         std::fprintf(stderr, "usage: svo_host_check io | fs W H CELL THR NUM BUCKET IMAGE [EX EY]... | fv W H CELL THR IMAGE\n");

@@ -252,3 +252,22 @@ def map_objects(p, levels=1, ctx=None, seed=0):
     for i, f in enumerate(p.cand_feat):
         m.add_new_candidate(feats[f], svo_amd.Point(p.cand_pos[i]))
     return m, ref, kf, cur, points, feats
+
+
+def write_map_problem(p, directory, cell_order):
+    """Files for build/svo_host_check map (the C++ mirror's Map): DATA.bin (doubles, layout in
+    host/svo_host_check.cpp) and the three base images.  Returns the four paths."""
+    import os
+    c = p.camera
+    parts = [[c["fx"], c["fy"], c["cx"], c["cy"], c["width"], c["height"], p.cell_size], p.ref_pose, p.kf_pose,
+             p.cur_pose, [p.n_ref, p.n_kf, len(p.point_pos), len(p.cand_feat), len(cell_order)], p.feat_px.ravel(),
+             p.feat_point, p.point_pos.ravel(), p.point_type, p.point_succ, p.cand_feat, p.cand_pos.ravel(),
+             cell_order]
+    data = np.concatenate([np.asarray(x, np.float64).ravel() for x in parts])
+    paths = [os.path.join(directory, n) for n in ("map.bin", "ref.raw", "kf.raw", "cur.raw")]
+    with open(paths[0], "wb") as f:
+        f.write(data.tobytes())
+    for path, img in zip(paths[1:], (p.ref_img, p.kf_img, p.cur_img)):
+        with open(path, "wb") as f:
+            f.write(np.ascontiguousarray(img, np.uint8).tobytes())
+    return paths

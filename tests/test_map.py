@@ -166,15 +166,8 @@ def test_gpu_cpp_mirror_map(tmp_path):
     W, H = c["width"], c["height"]
     ncells = math.ceil(W / mp.cell_size) * math.ceil(H / mp.cell_size)
     order = np.random.default_rng(5).permutation(ncells).astype(np.int32)
-    parts = [[c["fx"], c["fy"], c["cx"], c["cy"], W, H, mp.cell_size], mp.ref_pose, mp.kf_pose, mp.cur_pose,
-             [mp.n_ref, mp.n_kf, len(mp.point_pos), len(mp.cand_feat), ncells], mp.feat_px.ravel(), mp.feat_point,
-             mp.point_pos.ravel(), mp.point_type, mp.point_succ, mp.cand_feat, mp.cand_pos.ravel(), order]
-    data = np.concatenate([np.asarray(x, np.float64).ravel() for x in parts])
-    (tmp_path / "m.bin").write_bytes(data.tobytes())
-    for name, img in (("ref", mp.ref_img), ("kf", mp.kf_img), ("cur", mp.cur_img)):
-        (tmp_path / f"{name}.raw").write_bytes(np.ascontiguousarray(img).tobytes())
-    out = subprocess.run([exe, "map", str(tmp_path / "m.bin"), str(tmp_path / "ref.raw"), str(tmp_path / "kf.raw"),
-                          str(tmp_path / "cur.raw")], capture_output=True, text=True, timeout=60, check=True)
+    paths = synth.write_map_problem(mp, str(tmp_path), order)
+    out = subprocess.run([exe, "map", *paths], capture_output=True, text=True, timeout=60, check=True)
     lines = out.stdout.splitlines()
     got = np.array([[float(v) for v in l.split()[1:]] for l in lines[1:]]).reshape(-1, 2)
     grad = {k: O.unpack_levels(O.build_pyramid(img, 1)[1], W, H, 1)[0]
