@@ -192,3 +192,15 @@ def test_gpu_cpp_mirror_depth_estimator(problem, tmp_path):
     got = np.array([[float(v) for v in line.split()[1:]] for line in out[1:]]).reshape(-1, 3)
     assert got.shape == pts.shape
     np.testing.assert_allclose(got, pts, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_large_seed_set_pageable_staging():
+    """80k seeds (10 MB of per-call data, past the context's 8 MB pinned staging block): the pageable
+    staging path gives the oracle's answers."""
+    p = synth.make_depth_problem(n_seeds=2000)
+    seeds = O.make_seeds(p.px, p.bearing, p.depth_mean, p.depth_min)
+    seeds = np.concatenate([seeds] * 40)
+    g = gpu_update(p.camera, p.kf_img, p.kf_pose, p.cur_img, p.cur_pose, seeds)
+    c = O.depth_update(p.camera, [p.kf_img], p.kf_pose[None], p.cur_img, p.cur_pose, seeds)
+    check_same(g, c)

@@ -225,3 +225,22 @@ def test_feature_align_bitexact(patch):
     assert np.array_equal(np.isnan(err_g), np.isnan(err_c))
     ok = ~np.isnan(err_c)
     assert np.array_equal(err_g[ok], err_c[ok])
+
+
+def test_feature_align_large_batch_pageable_staging():
+    """200k candidates (11 MB of per-call data, past the context's 8 MB pinned staging block): the
+    pageable staging path gives the same bit-exact answers."""
+    s = synth.make_pair(n_features=2000, patch_size=7)
+    rng = np.random.default_rng(11)
+    reps = 100
+    ref_px = np.tile(s.px[:2000], (reps, 1))
+    init = ref_px + rng.uniform(-1.5, 1.5, ref_px.shape)
+    ref_grad = O.build_pyramid(s.ref_img, 1)[1]
+    cur_grad = O.build_pyramid(s.cur_img, 1)[1]
+    px_c, err_c, st_c = O.feature_align(s.camera, 7, ref_grad, cur_grad, ref_px, init)
+    ps = svo_amd.PyramidSet(2, 1241, 376, 1)
+    ps.upload(0, np.stack([s.ref_img, s.cur_img]))
+    ps.build()
+    px_g = np.ascontiguousarray(init.copy())
+    err_g, st_g = svo_amd.FeatureAlignment(7).align_batch(ps, 0, ps, 1, ref_px, px_g, svo_amd.PinholeCamera.kitti())
+    assert np.array_equal(px_g, px_c) and np.array_equal(st_g, st_c)
