@@ -352,12 +352,33 @@ def secondary(args, ctx, scene, cam, camera, reps=20):
     vpx, _, _ = O.feature_select_by_value(scene.ref_img, 50, 30)
     cv = time.perf_counter() - t0
     fr.image_pyramid.clear()
+    # the same calls through the C++ mirror (host/svo.hpp FeatureSelection via build/svo_host_check with
+    # SVO_CHECK_REPS): reported only when its features equal the oracle's
+    cpp_fs = {"fs": None, "fv": None}
+    exe = os.path.join(ROOT, "semi-direct-visual-odometry_amd", "build", "svo_host_check")
+    if os.path.exists(exe):
+        import subprocess
+        import tempfile
+        with tempfile.NamedTemporaryFile(suffix=".raw") as tf:
+            tf.write(np.ascontiguousarray(scene.ref_img, np.uint8).tobytes())
+            tf.flush()
+            W, H = str(cam["width"]), str(cam["height"])
+            for mode, argv, want in (("fs", [W, H, "30", "50", "200", "1", tf.name], opx), ("fv", [W, H, "30", "50", tf.name], vpx)):
+                r = subprocess.run([exe, mode, *argv], capture_output=True, text=True, timeout=120,
+                                   env=dict(os.environ, SVO_CHECK_REPS=str(reps)))
+                if r.returncode != 0:
+                    continue
+                got_cpp = np.array([[float(v) for v in ln.split()[:2]] for ln in r.stdout.splitlines()]).reshape(-1, 2)
+                ms = [ln for ln in r.stderr.splitlines() if ln.startswith("ms ")]
+                if ms and np.array_equal(got_cpp, want):
+                    cpp_fs[mode] = round(float(ms[-1].split()[1]), 4)
     res["feature_selection"] = {
         "keypoints": int(nk), "features": int(len(opx)), "gpu_ms_per_call": round(g * 1e3, 4),
         "detect_call_ms": round(det_ms, 4), "cpu_ms_1_thread": round(c * 1e3, 3),
         "bitexact_vs_oracle": bool(np.array_equal(got, opx)),
         "by_value_gpu_ms_per_call": round(gv * 1e3, 4), "by_value_cpu_ms_1_thread": round(cv * 1e3, 3),
         "by_value_bitexact_vs_oracle": bool(np.array_equal(gotv, vpx)),
+        "cpp_mirror_ms_per_call": cpp_fs["fs"], "by_value_cpp_mirror_ms_per_call": cpp_fs["fv"],
         "note": "gradientMagnitudeWithSSC end to end per keyframe (device detect + host sort/SSC, "
                 "Python mirror); ByValue: one device launch per call"}
     # BundleAdjustment::optimizePose for 512 frames of 1000 features each (85 % with a

@@ -55,17 +55,30 @@ int main(int argc, char** argv) {
             auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, 300.0, 300.0, w / 2.0, h / 2.0});
             auto frame = std::make_shared<Frame>(ctx, cam, img.data(), 1);
             FeatureSelection sel(ctx, w, h, cell);
-            if (mode == "fs") {
-                std::vector<std::shared_ptr<Feature>> existing;
+            std::vector<std::shared_ptr<Feature>> existing;
+            if (mode == "fs")
                 for (int i = 9; i + 1 < argc; i += 2)
                     existing.push_back(std::make_shared<Feature>(frame.get(), Vec2{std::atof(argv[i]), std::atof(argv[i + 1])}));
+            auto run = [&]() {
+                frame->m_features.clear();
+                sel.resetGridOccupancy();
                 sel.setExistingFeatures(existing);
-                sel.gradientMagnitudeWithSSC(frame, thr, std::atoi(argv[6]), std::atoi(argv[7]) != 0);
-            } else {
-                sel.gradientMagnitudeByValue(frame, thr, true);
-            }
+                if (mode == "fs") sel.gradientMagnitudeWithSSC(frame, thr, std::atoi(argv[6]), std::atoi(argv[7]) != 0);
+                else sel.gradientMagnitudeByValue(frame, thr, true);
+            };
+            run();
             for (const auto& f : frame->m_features)
                 std::printf("%.17g %.17g %.17g\n", f->m_pixelPosition[0], f->m_pixelPosition[1], f->m_gradientMagnitude);
+            // SVO_CHECK_REPS=n: time n more calls (selection only; the grid reset / existing features are
+            // inside the loop but cost nanoseconds) and report the average on stderr
+            const char* reps_env = std::getenv("SVO_CHECK_REPS");
+            const int reps = reps_env ? std::atoi(reps_env) : 0;
+            if (reps > 0) {
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int r = 0; r < reps; ++r) run();
+                const auto t1 = std::chrono::steady_clock::now();
+                std::fprintf(stderr, "ms %.6f\n", std::chrono::duration<double, std::milli>(t1 - t0).count() / reps);
+            }
             return 0;
         }
         if (mode == "ba" && argc >= 4) {
