@@ -31,6 +31,7 @@ import svo_amd.synth as synth  # noqa: E402
 
 METRIC = "frame-pair alignments/sec @2000 feats, 5-lvl pyramid; SE(3) err vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_VALU_PEAK_TFS = 78.6  # MI355X spec fp64 vector (half the 157.3 TF FP32 vector rate of MI355X_MICROARCH.md)
 
 
 def parse():
@@ -188,6 +189,14 @@ def main():
                      "algorithmic_bytes_per_pair": b_pair, "traffic_source": traffic_src,
                      "stages_ms": {k: round(v, 4) for k, v in stages.items()},
                      "dominant_stage": max(stages, key=stages.get)},
+        # the co-limiting roof SURVEY 8(d) names: ~1900 algorithmic fp64 flop per feature and level
+        # (bilinear blends, Jacobian, SE3 / projection, weights, 5 factored accumulators, 21 x 3 expansion)
+        "roofline_fp64_valu": {"achieved": round(1900.0 * nf * L * P / (kernel_ms * 1e-3) / 1e12, 3),
+                               "peak": FP64_VALU_PEAK_TFS, "unit": "TFLOP/s",
+                               "frac": round(1900.0 * nf * L * P / (kernel_ms * 1e-3) / 1e12 / FP64_VALU_PEAK_TFS, 5),
+                               "flop_per_pair": 1900 * nf * L,
+                               "note": "algorithmic flops (SURVEY 8(d) estimate); the issued VALU instructions are "
+                                       "several times more (address, conversion, select): DESIGN 7 SQ counters"},
         "pyramid_build": {"frames": 3 * P, "ms": round(pyr_ms, 4),
                           "frames_per_s": round(3 * P / (pyr_ms * 1e-3), 1),
                           # algorithmic bytes per frame: read the base image once, write the gradient
