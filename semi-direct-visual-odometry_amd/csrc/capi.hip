@@ -69,6 +69,10 @@ struct svo_ctx {
     // pinned host staging of the same calls (fixed size, ctx_pinned): one H2D and one D2H copy per call
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
+    // svo_align_batch_set_pair stages into the same block as a ring without waiting for its copies;
+    // every other user of the block first drains them (ctx_pinned)
+    size_t ring_off = 0;
+    bool ring_pending = false;
 };
 
 // at least `bytes` of the context's scratch (the previous contents are not kept)
@@ -91,8 +95,28 @@ static hipError_t ctx_scratch(svo_ctx* c, size_t bytes, void** out) {
 // one failed with "invalid argument").  Calls whose payload exceeds it (or when pinning fails) stage in
 // pageable memory or copy straight from the caller's arrays.
 constexpr size_t kPinnedCap = (size_t)8 << 20;
+static hipError_t ctx_pinned_alloc(svo_ctx* c) {
+    if (c->pinned) return hipSuccess;
+    const hipError_t e = hipHostMalloc(&c->pinned, kPinnedCap, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        c->pinned = nullptr;
+        return e;
+    }
+    c->pinned_bytes = kPinnedCap;
+    return hipSuccess;
+}
+
+static hipError_t ctx_ring_drain(svo_ctx* c) {
+    if (!c->ring_pending) return hipSuccess;
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    c->ring_pending = false;
+    c->ring_off = 0;
+    return e;
+}
+
 static hipError_t ctx_pinned(svo_ctx* c, size_t bytes, void** out) {
     if (bytes > kPinnedCap) return hipErrorInvalidValue;
+    if (hipError_t e = ctx_ring_drain(c)) return e;
     if (!c->pinned) {
         const hipError_t e = hipHostMalloc(&c->pinned, kPinnedCap, hipHostMallocDefault);
         if (e != hipSuccess) {
@@ -423,15 +447,44 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
     d.n_ref = n_ref;
     d.n_kf = n_kf;
     const size_t fo = (size_t)pair * b->max_f;
-    hipStream_t s = b->ctx->stream;
-    if (nf > 0) {
-        SVO_HIP(hipMemcpyAsync(b->d_px + 2 * fo, px, nf * 2 * sizeof(double), hipMemcpyHostToDevice, s));
-        SVO_HIP(hipMemcpyAsync(b->d_bearing + 3 * fo, bearing, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
-        SVO_HIP(hipMemcpyAsync(b->d_point + 3 * fo, point, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
-        SVO_HIP(hipMemcpyAsync(b->d_has_point + fo, has_point, nf, hipMemcpyHostToDevice, s));
+    svo_ctx* c = b->ctx;
+    hipStream_t s = c->stream;
+    // stage the pair's arrays in the context's pinned ring and return without waiting: the copies are
+    // ordered before any later work on the stream, and the ring drains when it wraps or another call
+    // needs the pinned block (large pairs, or no pinned memory: direct copies and a wait, as before)
+    auto r8 = [](size_t v) { return (v + 7) / 8 * 8; };
+    const size_t n = (size_t)nf;
+    const size_t need = r8(sizeof(d)) + n * 16 + n * 24 * 2 + r8(n);
+    if (need <= kPinnedCap && ctx_pinned_alloc(c) == hipSuccess) {
+        if (c->ring_off + need > kPinnedCap) SVO_HIP(ctx_ring_drain(c));
+        char* h = static_cast<char*>(c->pinned) + c->ring_off;
+        std::memcpy(h, &d, sizeof(d));
+        char* hp = h + r8(sizeof(d));
+        if (nf > 0) {
+            std::memcpy(hp, px, n * 16);
+            std::memcpy(hp + n * 16, bearing, n * 24);
+            std::memcpy(hp + n * 40, point, n * 24);
+            std::memcpy(hp + n * 64, has_point, n);
+            SVO_HIP(hipMemcpyAsync(b->d_px + 2 * fo, hp, n * 16, hipMemcpyHostToDevice, s));
+            SVO_HIP(hipMemcpyAsync(b->d_bearing + 3 * fo, hp + n * 16, n * 24, hipMemcpyHostToDevice, s));
+            SVO_HIP(hipMemcpyAsync(b->d_point + 3 * fo, hp + n * 40, n * 24, hipMemcpyHostToDevice, s));
+            SVO_HIP(hipMemcpyAsync(b->d_has_point + fo, hp + n * 64, n, hipMemcpyHostToDevice, s));
+        }
+        SVO_HIP(hipMemcpyAsync(b->d_pairs + pair, h, sizeof(d), hipMemcpyHostToDevice, s));
+        c->ring_off += need;
+        c->ring_pending = true;
+    } else {
+        (void)hipGetLastError();
+        SVO_HIP(ctx_ring_drain(c));
+        if (nf > 0) {
+            SVO_HIP(hipMemcpyAsync(b->d_px + 2 * fo, px, nf * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+            SVO_HIP(hipMemcpyAsync(b->d_bearing + 3 * fo, bearing, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+            SVO_HIP(hipMemcpyAsync(b->d_point + 3 * fo, point, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+            SVO_HIP(hipMemcpyAsync(b->d_has_point + fo, has_point, nf, hipMemcpyHostToDevice, s));
+        }
+        SVO_HIP(hipMemcpyAsync(b->d_pairs + pair, &d, sizeof(d), hipMemcpyHostToDevice, s));
+        SVO_HIP(hipStreamSynchronize(s));
     }
-    SVO_HIP(hipMemcpyAsync(b->d_pairs + pair, &d, sizeof(d), hipMemcpyHostToDevice, s));
-    SVO_HIP(hipStreamSynchronize(s));
     b->pair_set[pair] = 1;
     return SVO_OK;
 }
