@@ -8,15 +8,20 @@ path over one batch: --pairs independent pairs per GPU (default 512), inputs (py
 poses) resident in HBM before the timed region.  Data: synthetic street scenes (svo_amd.synth, seeds
 0x5EED0000 + global pair index modulo --distinct), each pair in its own HBM buffers.
 
-Multi-GPU: one process per GPU (torch.distributed.run); pairs are independent, so each rank aligns its
-own --pairs (weak scaling) and there is no data-path collective: the gloo process group is used only
-for the barrier and the max-over-ranks time.
+Multi-GPU: one process per GPU; pairs are independent, so each rank aligns its own --pairs (weak
+scaling) and there is no data-path collective: the gloo process group is used only for the barrier and
+the max-over-ranks time.  Under torch.distributed.run the ranks come from RANK / LOCAL_RANK / WORLD_SIZE
+(which must equal --gpus); `python bench.py --gpus N` without them starts the N ranks itself (child
+processes on 127.0.0.1, before anything touches the GPU) and exits with their status.  --cpu-rehearsal
+runs the same launcher / barrier / max-over-ranks path with the CPU oracle as the step (tests only).
 
 Prints one JSON line (rank 0).  See DESIGN.md §Measurement for the roofline and baseline definitions.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,10 +52,15 @@ def parse():
     ap.add_argument("--feature-order", choices=("cell", "shuffled"), default="cell",
                     help="cell: features in the order the reference detector emits them (30-px grid cells row by "
                          "row, src/feature_selection.cpp:103-141); shuffled: random order")
+    ap.add_argument("--median", choices=("reference", "exact"), default="exact",
+                    help="robust-scale semantics: reference = the reference's libstdc++ nth_element post-state "
+                         "(median_mode SVO_MEDIAN_REFERENCE, K2R); exact = true order statistics (K2)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the single-core CPU baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-core CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the config 3 / config 5 lines")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="no GPU: each rank's step is the CPU oracle on its pairs (exercises the multi-rank path)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC traffic summary of this workload (tools/pmc_traffic.py output)")
     return ap.parse_args()
@@ -75,15 +85,40 @@ def level_bytes(w, h, levels):
     return tot
 
 
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """Start n ranks of this script as child processes (one per GPU) and wait for all of them; the parent
+    never touches the GPU.  Returns the worst exit status."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: E402  (gloo: host-side barrier / max only)
         dist.init_process_group(backend="gloo")
+    if args.cpu_rehearsal:
+        return rehearsal(args, rank, world, dist)
 
     ctx = svo_amd.Context(local_rank)
     P, nf, L, patch = args.pairs, args.features, args.levels, args.patch
@@ -110,7 +145,8 @@ def main():
     pyr_bytes = 2 * cam["width"] * cam["height"] + 2 * (level_bytes(cam["width"], cam["height"], L)
                                                        - cam["width"] * cam["height"])
 
-    batch = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx)
+    mode = svo_amd.MEDIAN_REFERENCE if args.median == "reference" else svo_amd.MEDIAN_EXACT
+    batch = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx, median_mode=mode)
     for i in range(P):
         s = scenes[i % D]
         batch.set_pair(i, (ps, 3 * i), (ps, 3 * i + 1), (ps, 3 * i + 2), s.ref_pose, s.kf_pose, s.cur_init_pose,
@@ -229,6 +265,52 @@ def main():
     if not args.no_cpu and world == 1:
         out.update(cpu_baseline(args, scenes, poses, L, patch, nthreads))
     print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def rehearsal(args, rank, world, dist):
+    """The multi-rank path without a GPU: each rank's step aligns its --pairs with the CPU oracle (tests)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # noqa: E402  (rehearsal only)
+    P, nf, L, patch = args.pairs, args.features, args.levels, args.patch
+    first, _ = shard.pair_block(world * P, rank, world)
+    scenes = [synth.make_pair(seed=synth.SEED_BASE + first + i, n_features=nf, patch_size=patch, nthreads=1)
+              for i in range(P)]
+    pairs = []
+    for s in scenes:
+        pyr = [O.build_pyramid(im, L)[0] for im in (s.ref_img, s.kf_img, s.cur_img)]
+        pairs.append(O.make_pair(pyr[0], pyr[1], pyr[2], s.ref_pose, s.kf_pose, s.n_ref, s.n_kf, s.px, s.bearing,
+                                 s.point, s.has_point))
+
+    def step():
+        return [O.image_align(s.camera, patch, 0, L - 1, pr, s.cur_init_pose, 0)[0] for s, pr in zip(scenes, pairs)]
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        poses = step()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        gathered = shard.gather_blocks([list(map(float, p)) for p in poses], dist)
+    else:
+        gathered = [list(map(float, p)) for p in poses]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(world * P * args.steps / elapsed, 3), "unit": "pairs/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "cpu rehearsal (no GPU)",
+                          "config": {"workload": "rehearsal", "pairs_per_gpu": P, "features": nf, "levels": L},
+                          "poses": gathered}), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()

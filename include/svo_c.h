@@ -60,9 +60,17 @@ typedef struct {
     int32_t width, height;
 } svo_camera;
 
+/* Robust-scale semantics of the Tukey weights (Optimizer::tukeyWeighting, src/optimizer.cpp:485-514, with
+ * algorithm::computeMedian / computeMAD, src/algorithm.cpp:834-865).
+ *   SVO_MEDIAN_REFERENCE: the reference's own values: std::nth_element on the full residual vector and,
+ *     for an even length, vec[n/2 - 1] as libstdc++'s introselect leaves it (not always the (n/2 - 1)-th
+ *     order statistic): the device re-runs the introselect (K2R, csrc/align_ref.hip);
+ *   SVO_MEDIAN_EXACT: true order statistics ((n/2 - 1)-th and n/2-th), the robust statistic the
+ *     reference means; faster (K2). */
+enum { SVO_MEDIAN_EXACT = 0, SVO_MEDIAN_REFERENCE = 1 };
+
 /* ImageAlignment(patchSize, minLevel, maxLevel, numParameters=6) (include/image_alignment.hpp:18).
- * median_mode: 0 = exact order statistics for the Tukey scale (the only mode implemented; the
- * reference's libstdc++ nth_element neighbour read is within the pose tolerance). */
+ * median_mode: SVO_MEDIAN_EXACT or SVO_MEDIAN_REFERENCE (above). */
 typedef struct {
     int32_t patch_size;
     int32_t min_level;
@@ -149,6 +157,12 @@ int svo_align_batch_profile(svo_align_batch* batch, float* stage_ms);
 int svo_align_batch_results(svo_align_batch* batch, double* poses, double* err, int32_t* status);
 /* Per-level records of one pair (max_level+1 entries, indexed by level). */
 int svo_align_batch_traces(svo_align_batch* batch, int32_t pair, svo_level_trace* out);
+
+/* Diagnostics (no reference counterpart): the SVO_MEDIAN_REFERENCE robust scale of an arbitrary residual
+ * vector, i.e. algorithm::computeMAD(values, n_valid) (src/algorithm.cpp:855-865) and the median it uses, on
+ * the device.  values: n_slots entries in [-255, 255] or DBL_MAX (an invisible slot); med_mad[0] = median,
+ * med_mad[1] = MAD.  Synchronous. */
+int svo_debug_robust_scale(svo_ctx* ctx, const double* values, int64_t n_slots, int64_t n_valid, double* med_mad);
 
 /* ---------------------------------------------------------------- FeatureAlignment
  * Replaces FeatureAlignment::align(refFeature, curFrame, pixelPos) (src/feature_alignment.cpp:25-62,

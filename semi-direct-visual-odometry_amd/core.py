@@ -292,16 +292,24 @@ def _feature_arrays(frames):
     return px, br, pt, hp
 
 
-class AlignBatch:
-    """n_pairs independent ImageAlignment::align problems on one GPU (svo_align_batch)."""
+MEDIAN_EXACT, MEDIAN_REFERENCE = 0, 1  # include/svo_c.h SVO_MEDIAN_*
 
-    def __init__(self, camera, patch_size, min_level, max_level, n_pairs, max_features, ctx=None):
+
+class AlignBatch:
+    """n_pairs independent ImageAlignment::align problems on one GPU (svo_align_batch).
+
+    median_mode: MEDIAN_REFERENCE reproduces the reference's robust scale bit for bit (libstdc++
+    nth_element post-state, src/algorithm.cpp:834-853); MEDIAN_EXACT uses true order statistics."""
+
+    def __init__(self, camera, patch_size, min_level, max_level, n_pairs, max_features, ctx=None,
+                 median_mode=MEDIAN_EXACT):
         self.ctx = ctx or default_context()
         self.camera = camera
         self.n_pairs = int(n_pairs)
         self.max_level = int(max_level)
+        self.median_mode = int(median_mode)
         self._c_cam = camera.as_c()
-        self._c_prm = _capi.SvoAlignParams(int(patch_size), int(min_level), int(max_level), 0)
+        self._c_prm = _capi.SvoAlignParams(int(patch_size), int(min_level), int(max_level), self.median_mode)
         h = ctypes.c_void_p()
         check(lib().svo_align_batch_create(self.ctx.handle, ctypes.byref(self._c_cam), ctypes.byref(self._c_prm),
                                            self.n_pairs, int(max_features), ctypes.byref(h)))
@@ -731,6 +739,17 @@ class FeatureSelection:
                                                 ptr(resp), ctypes.byref(n)))
         self.occupancy_grid[:] = occ
         return self._emit(frame, px, resp, n.value)
+
+
+def debug_robust_scale(values, n_valid, ctx=None):
+    """svo_debug_robust_scale: algorithm::computeMAD(values, n_valid) with the reference's libstdc++
+    nth_element post-state (MEDIAN_REFERENCE), on the device; returns (median, mad).  values: the full
+    residual vector, invisible slots = DBL_MAX (src/optimizer.cpp:387-396)."""
+    ctx = ctx or default_context()
+    v = np.ascontiguousarray(values, np.float64)
+    out = np.zeros(2)
+    check(lib().svo_debug_robust_scale(ctx.handle, ptr(v), len(v), int(n_valid), ptr(out)))
+    return float(out[0]), float(out[1])
 
 
 # ---------------------------------------------------------------- pose-only bundle adjustment

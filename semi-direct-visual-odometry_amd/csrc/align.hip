@@ -25,8 +25,11 @@
 //                fixed order (deterministic, no float atomics) and takes the LM step: Nielsen damping,
 //                Eigen-LDLT, pose <- pose * exp(-dx), status, RMSE (src/optimizer.cpp:279-366,
 //                src/image_alignment.cpp:379)
+#include <type_traits>
+
 #include "svo_internal.h"
 #include "svo_math.h"
+#include "svo_wave.h"
 
 namespace svo {
 
@@ -46,58 +49,6 @@ constexpr int kRankCap = 256;        // <= this many candidates: rank counting, 
 constexpr int kPrevCap = 256;        // slots of the bin below the median's gathered for its lower neighbour
 constexpr int kRadixBits = 11;
 constexpr double kDblMax = 1.7976931348623157e308;
-
-// Wave reductions and scans with DPP row operations (GFX9 encodings) instead of shfl (ds_bpermute, an
-// LDS round trip per step): quad_perm / row_half_mirror / row_mirror reduce inside each 16-lane row,
-// readlane combines the four rows.  DPP reads every lane's register regardless of EXEC, so all 64 lanes
-// must be active: every caller is block-uniform code.
-template <int kCtrl>
-__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
-}
-template <int kCtrl>
-__device__ __forceinline__ double dpp_mov(double v) {
-    const uint2 u = __builtin_bit_cast(uint2, v);
-    return __builtin_bit_cast(double, make_uint2(dpp_mov<kCtrl>(u.x), dpp_mov<kCtrl>(u.y)));
-}
-__device__ __forceinline__ uint32_t lane_read(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-__device__ __forceinline__ double lane_read(double v, int l) {
-    const uint2 u = __builtin_bit_cast(uint2, v);
-    return __builtin_bit_cast(double, make_uint2(lane_read(u.x, l), lane_read(u.y, l)));
-}
-template <typename T, typename F>
-__device__ __forceinline__ T wave_allreduce(T v, F op) {
-    v = op(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
-    v = op(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
-    v = op(v, dpp_mov<0x141>(v));  // row_half_mirror
-    v = op(v, dpp_mov<0x140>(v));  // row_mirror: every lane of a row holds the row's result
-    return op(op(lane_read(v, 0), lane_read(v, 16)), op(lane_read(v, 32), lane_read(v, 48)));
-}
-__device__ __forceinline__ uint32_t wave_sum_u(uint32_t v) {
-    return wave_allreduce(v, [](uint32_t x, uint32_t y) { return x + y; });
-}
-__device__ __forceinline__ uint32_t wave_min_u(uint32_t v) {
-    return wave_allreduce(v, [](uint32_t x, uint32_t y) { return x < y ? x : y; });
-}
-__device__ __forceinline__ uint32_t wave_max_u(uint32_t v) {
-    return wave_allreduce(v, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
-}
-__device__ __forceinline__ double wave_max(double v) {
-    return wave_allreduce(v, [](double x, double y) { return fmax(x, y); });
-}
-// inclusive prefix sum over the wave: row_shr 1..3 (bound_ctrl zero-fills across the row start), row_shr
-// 4 / 8 into banks 1-3 / 2-3, then row_bcast 15 / 31 carry the row totals into rows 1, 3 / 2, 3
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    uint32_t s = v;
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xF, 0xF, true);
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x114, 0xF, 0xE, true);
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x118, 0xF, 0xC, true);
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xA, 0xF, false);
-    s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xC, 0xF, false);
-    return s;
-}
 
 // Window geometry of one feature at one level (patch half size kHalf), in image cells relative to
 // (floor(u), floor(v)) of the feature at that level.
@@ -316,14 +267,19 @@ __device__ __forceinline__ V3 world_point(const AlignArgs& a, const PairDesc& P,
 // are formed once and shared by the two patch rows that read them: bit-identical to the per-sample
 // formula whenever x1 = floor(u) + kx and y1 = floor(v) + ky.  A feature where u + kx rounds up to the
 // next integer (x1 = floor(u) + kx + 1) takes the per-pixel path instead.
-template <int kHalf, bool kWin>  // kWin: a window level (AlignArgs::win_levels)
+// kRef (median_mode SVO_MEDIAN_REFERENCE): 32-bit keys (res_key32) in the reference's feature-major slot
+// order (slot f * area + k, the order K2R's introselect runs over) instead of 16-bit pixel-major ones.
+template <int kHalf, bool kWin, bool kRef>  // kWin: a window level (AlignArgs::win_levels)
 __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual_kernel(AlignArgs a, int level) {
     using G = Win<kHalf>;
+    using KeyT = typename std::conditional<kRef, uint32_t, uint16_t>::type;
     constexpr int h = G::h, side = G::side, RB = G::RB, NW = G::RW;
-    // keys are staged in LDS as [pixel][feature] and written as whole 16-B pieces of the slot rows (one
-    // 2-B store per lane and pixel wrote each 128-B line in many partial requests: 2.8x the key bytes)
-    constexpr bool kLds = G::A * kLaneFeats * 2 <= 32768;
-    __shared__ __attribute__((aligned(16))) uint16_t kbuf[kLds ? G::A : 1][kLaneFeats];
+    constexpr KeyT kInvis = kRef ? (KeyT)kKeyInvisible : (KeyT)0xFFFF;
+    // keys are staged in LDS ([pixel][feature], or [feature][pixel] for kRef) and written as whole 16-B
+    // pieces of the slot rows (one 2-B store per lane and pixel wrote each 128-B line in many partial
+    // requests: 2.8x the key bytes)
+    constexpr bool kLds = G::A * kLaneFeats * (int)sizeof(KeyT) <= 32768;
+    __shared__ __attribute__((aligned(16))) KeyT kbuf[kLds ? G::A * kLaneFeats : 1];
     int pair, chunk;
     xcd_pair_chunk(a.chunks, pair, chunk);
     if (pair >= a.n_pairs) return;
@@ -341,12 +297,22 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
     const int64_t loff = a.geom.off[level];
     const double scale = ldexp(1.0, -level);  // = 1 / 2^level exactly, no division
     const int border = h + 2;
-    // key of slot (k, f) at keys[k * fstride + f]
+    // key of slot (k, f) at keys[k * fstride + f] (kRef: keys32[f * area + k])
     const __amdgpu_buffer_rsrc_t keys = slot_rsrc(a.keys + (int64_t)pair * a.key_stride, a.key_stride * 2);
     const uint32_t fo = (uint32_t)f;
-    auto put = [&](int k, uint16_t key) {
-        if constexpr (kLds) kbuf[k][tid] = key;
-        else slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), key);
+    auto put = [&](int k, KeyT key) {
+        if constexpr (kLds) {
+            if constexpr (kRef) kbuf[tid * G::A + k] = key;
+            else kbuf[k * kLaneFeats + tid] = key;
+        } else if constexpr (kRef) {
+            a.keys32[(int64_t)pair * a.key_stride + (int64_t)f * G::A + k] = key;
+        } else {
+            slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), key);
+        }
+    };
+    auto rkey = [](double r) -> KeyT {
+        if constexpr (kRef) return res_key32(r);
+        else return res_key(r);
     };
     int vis = 0;
     double ur = 0.0, vr = 0.0, cu = 0.0, cv = 0.0;
@@ -382,7 +348,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
     if (vis != 3) {
         if (f < fstride) {
 #pragma unroll
-            for (int k = 0; k < G::A; ++k) put(k, 0xFFFF);
+            for (int k = 0; k < G::A; ++k) put(k, kInvis);
         }
     } else {
         const uint8_t* const rplane = (f < P.n_ref ? P.ref_pyr : P.kf_pyr) + loff;
@@ -445,7 +411,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
                     for (int kx = 0; kx < side; ++kx) {  // (y2 - y) a + (y - y1) b
                         const double T = (1.0 - rwy) * rprev[kx] + rwy * rcur[kx];
                         const double I = (1.0 - cwy) * cprev[kx] + cwy * ccur[kx];
-                        put(ky * side + kx, res_key(I - T));
+                        put(ky * side + kx, rkey(I - T));
                     }
                 }
 #pragma unroll
@@ -456,18 +422,24 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
                 for (int kx = 0; kx < side; ++kx) {
                     const double T = bilinear_d(rplane, W, ur + (double)(kx - h), vr + (double)(ky - h));
                     const double I = bilinear_d(cplane, W, cu + (double)(kx - h), cv + (double)(ky - h));
-                    put(ky * side + kx, res_key(I - T));
+                    put(ky * side + kx, rkey(I - T));
                 }
         }
     }
-    if constexpr (kLds) {
+    if constexpr (kLds && kRef) {  // the workgroup's features are one contiguous run of slots
+        __syncthreads();
+        const int nfe = fstride - f0 < kLaneFeats ? fstride - f0 : kLaneFeats;  // a multiple of 64
+        uint32_t* const kp = a.keys32 + (int64_t)pair * a.key_stride + (int64_t)f0 * G::A;
+        for (int idx = tid; idx < nfe * G::A / 4; idx += kLaneFeats)
+            *reinterpret_cast<uint4*>(kp + 4 * idx) = *reinterpret_cast<const uint4*>(&kbuf[4 * idx]);
+    } else if constexpr (kLds) {
         __syncthreads();
         const int per_row = (fstride - f0 < kLaneFeats ? fstride - f0 : kLaneFeats) / 8;  // 16-B pieces
         uint16_t* const kp = a.keys + (int64_t)pair * a.key_stride + f0;
         for (int idx = tid; idx < G::A * per_row; idx += kLaneFeats) {
             const int k = idx / per_row, c8 = idx - k * per_row;
             *reinterpret_cast<uint4*>(kp + (int64_t)k * fstride + 8 * c8) =
-                *reinterpret_cast<const uint4*>(&kbuf[k][8 * c8]);
+                *reinterpret_cast<const uint4*>(&kbuf[k * kLaneFeats + 8 * c8]);
         }
     }
 }
@@ -1424,10 +1396,17 @@ static void launch_all(const AlignArgs& a, hipStream_t s, hipEvent_t* marks) {
     for (int level = a.max_level; level >= a.min_level; --level) {
         mark();
         const bool win = (a.win_levels >> level) & 1u;
-        if (win) hipLaunchKernelGGL((align_residual_kernel<kHalf, true>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
-        else hipLaunchKernelGGL((align_residual_kernel<kHalf, false>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
-        mark();
-        hipLaunchKernelGGL(align_scale_kernel, dim3(a.n_pairs), dim3(kSelThreads), 0, s, a, level);
+        if (a.median_mode == 1) {
+            if (win) hipLaunchKernelGGL((align_residual_kernel<kHalf, true, true>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+            else hipLaunchKernelGGL((align_residual_kernel<kHalf, false, true>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+            mark();
+            launch_scale_ref(a, level, s);
+        } else {
+            if (win) hipLaunchKernelGGL((align_residual_kernel<kHalf, true, false>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+            else hipLaunchKernelGGL((align_residual_kernel<kHalf, false, false>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
+            mark();
+            hipLaunchKernelGGL(align_scale_kernel, dim3(a.n_pairs), dim3(kSelThreads), 0, s, a, level);
+        }
         mark();
         if (win) hipLaunchKernelGGL((align_weights_kernel<kHalf, true>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);
         else hipLaunchKernelGGL((align_weights_kernel<kHalf, false>), dim3(fgrid), dim3(kLaneFeats), 0, s, a, level);

@@ -33,7 +33,7 @@ def oracle_align(s, patch, min_level, max_level, mode=0, trace=True, init=None):
                          s.cur_init_pose if init is None else init, median_mode=mode, trace=trace)
 
 
-def gpu_batch(pairs, patch, min_level, max_level, ctx=None, max_features=None):
+def gpu_batch(pairs, patch, min_level, max_level, ctx=None, max_features=None, median_mode=svo_amd.MEDIAN_EXACT):
     """Upload every pair (3 frames each) into one PyramidSet and one AlignBatch; returns (batch, set)."""
     cam = pairs[0].camera
     camera = svo_amd.PinholeCamera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"])
@@ -42,7 +42,7 @@ def gpu_batch(pairs, patch, min_level, max_level, ctx=None, max_features=None):
     ps.upload(0, imgs)
     ps.build()
     mf = max_features or max(max(len(s.px) for s in pairs), 1)
-    b = svo_amd.AlignBatch(camera, patch, min_level, max_level, len(pairs), mf, ctx)
+    b = svo_amd.AlignBatch(camera, patch, min_level, max_level, len(pairs), mf, ctx, median_mode=median_mode)
     for i, s in enumerate(pairs):
         b.set_pair(i, (ps, 3 * i), (ps, 3 * i + 1), (ps, 3 * i + 2), s.ref_pose, s.kf_pose, s.cur_init_pose,
                    s.n_ref, s.n_kf, s.px, s.bearing, s.point, s.has_point)
