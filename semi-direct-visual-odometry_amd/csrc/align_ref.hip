@@ -27,8 +27,13 @@
 // pass compares |r - median| through the keys' residual intervals and four key thresholds per pivot.
 // Round 1 streams K1's feature-major keys (16-B loads); the surviving segment goes to LDS (keys + 16-bit
 // ids when the vector has <= 65536 slots) when it fits, else to the pair's global scratch (sel) until it
-// does.  A round classifies every element once, keeping per-64-position-step GE / LE ballots; the scans,
-// the crossing, L_{Ks+1} / R_{Ks} and each swap's partners come from those records (four barriers).
+// does.  A round classifies every element once, keeping per-64-position-step GE / LE ballots in the
+// registers of the wave that owns the step; the scans, the crossing, L_{Ks+1} / R_{Ks} and each swap's
+// partners come from those records.  Segments of <= 64 steps run on one wave without barriers.
+//
+// Code size matters: the pass (median / MAD) and the segment's storage are runtime values, each phase is
+// compiled once (only the innermost loops are specialised), so the kernel's hot code stays inside the
+// instruction cache.
 #include "svo_internal.h"
 #include "svo_math.h"
 #include "svo_wave.h"
@@ -37,10 +42,10 @@ namespace svo {
 
 namespace {
 
-constexpr int kRT = 1024;              // threads per pair
+constexpr int kRT = 512;               // threads per pair
 constexpr int kRW = kRT / 64;          // waves
 constexpr int kMeta = 1024;            // LDS step records (64 positions each): segments up to 65536
-constexpr int kBatch = 4;              // sweeps: 256-position groups whose loads a wave issues before using any
+constexpr int kBatch = 4;              // loads a lane issues before using any (copies, swaps)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr double kDblMax = 1.7976931348623157e308;
 
@@ -55,6 +60,9 @@ struct Pivot {
     int inv;                 // pass 1: the pivot is DBL_MAX (an invisible slot)
     double plo, phi;         // pass 1: |r - med| interval of the pivot (equal: exact)
     int64_t kA, kB, kC, kD;  // pass 1: key-grid thresholds (see classify)
+    // branch-free fast classification (see fast_cls): the pivot's key, and for pass 1 the key ranges
+    // [tA, tB] (certainly |r - med| < plo), <= tC or >= tD (certainly > phi), the class of an invisible key
+    uint32_t tA, tB, tC, tD, inv_c;
 };
 
 template <typename Id>
@@ -63,13 +71,14 @@ struct RefShared {
     alignas(16) uint32_t key[kCap];          // the segment, from position `base`
     Id id[kCap];
     uint16_t lp[kCap / 2], rp[kCap / 2];     // L_k, R_k - b0 for k <= Ks (LDS rounds)
-    uint64_t mge[kMeta], mle[kMeta];         // per 64-position step: GE / LE ballots
-    uint32_t gpre[kMeta], lsuf[kMeta];       // GE before the step; LE from the step's start on
+    uint64_t mge[kMeta], mle[kMeta];         // per 64-position step: GE / LE ballots (for the crossing search)
     uint32_t wsum[kRW][2];
+    Pivot piv;
     uint32_t ks, cut_l, cut_r, l_ks;
-    El fin[3];
-    uint64_t stamp[32];  // diagnostics (svo_debug_robust_scale): per pass: cycles of round 1, of the rest, rounds;
-                         // then cycles per (round kind, phase) summed over both passes
+    uint32_t bc_first, bc_last, bc_depth, bc_rec;
+    El lo_el, fin[3];
+    uint64_t stamp[32];  // diagnostics (svo_debug_robust_scale): per pass: cycles of round 1, of the rest,
+                         // block rounds, wave rounds; [8..] cycles per phase of block rounds; [28..] exact calls
 };
 
 // where the current segment lives
@@ -77,14 +86,16 @@ enum { kSrc = 0, kGlb = 1, kLds = 2 };
 
 // ---- element sources: round-1 keys in the reference's order, and the exact residual of a slot
 struct ImgSrc {  // production: K1's keys and the images
-    const uint32_t* keys;   // pair's feature-major keys: slot f * area + k (padded: 16-B reads past M are safe)
+    using KeyBase = const uint32_t*;
+    static __device__ __forceinline__ uint32_t key_at(KeyBase kb, uint32_t p) { return kb[p]; }
+    const uint32_t* keys;   // pair's feature-major keys: slot f * area + k (padded)
     const double* px;       // pair's feature pixels (level 0)
     const double* cproj;    // pair's projections into the cur level (K1)
     const uint8_t *rplane, *kplane, *cplane;
     int W, area, side, half, n_ref;
     double scale;
     __device__ __forceinline__ uint32_t key(uint32_t p) const { return keys[p]; }
-    __device__ __forceinline__ uint4 key4(uint32_t p) const { return *reinterpret_cast<const uint4*>(keys + p); }
+    __device__ __forceinline__ KeyBase kbase() const { return keys; }
     // r = bilerpD(I_cur, cu + kx, cv + ky) - bilerpD(I_ref, u + kx, v + ky)  (src/image_alignment.cpp:351-359)
     __device__ double r(uint32_t s) const {
         const int f = (int)(s / (uint32_t)area), k = (int)s - f * area;
@@ -96,15 +107,21 @@ struct ImgSrc {  // production: K1's keys and the images
         return I - T;
     }
 };
-struct ArrSrc {  // svo_debug_robust_scale: an arbitrary residual vector (>= DBL_MAX = invisible), padded
+struct ArrSrc {  // svo_debug_robust_scale: an arbitrary residual vector (>= DBL_MAX = invisible), its keys
+    using KeyBase = const uint32_t*;
+    static __device__ __forceinline__ uint32_t key_at(KeyBase kb, uint32_t p) { return kb[p]; }
     const double* v;
-    __device__ __forceinline__ uint32_t key(uint32_t p) const { return v[p] >= kDblMax ? kKeyInvisible : res_key32(v[p]); }
-    __device__ __forceinline__ uint4 key4(uint32_t p) const { return make_uint4(key(p), key(p + 1), key(p + 2), key(p + 3)); }
+    const uint32_t* keys;
+    __device__ __forceinline__ uint32_t key(uint32_t p) const { return keys[p]; }
+    __device__ __forceinline__ KeyBase kbase() const { return keys; }
     __device__ __forceinline__ double r(uint32_t s) const { return v[s]; }
 };
 
 __device__ __forceinline__ int lg2(uint32_t n) { return 31 - __builtin_clz(n); }
-
+__device__ __forceinline__ uint64_t low_mask(uint32_t b) { return b >= 64 ? ~0ull : ((1ull << b) - 1ull); }
+__device__ __forceinline__ uint64_t lane_read_u64(uint64_t v, int l) {
+    return ((uint64_t)lane_read((uint32_t)(v >> 32), l) << 32) | lane_read((uint32_t)v, l);
+}
 // position of the j-th (0-based) set bit of m
 __device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t j) {
     uint32_t pos = 0;
@@ -115,86 +132,171 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t j) {
     }
     return pos;
 }
-// bits 0..15 of v to bits 0, 4, 8, .., 60
-__device__ __forceinline__ uint64_t spread4(uint64_t v) {
-    uint64_t x = v & 0xFFFFull;
-    x = (x | (x << 24)) & 0x000000FF000000FFull;
-    x = (x | (x << 12)) & 0x000F000F000F000Full;
-    x = (x | (x << 6)) & 0x0303030303030303ull;
-    x = (x | (x << 3)) & 0x1111111111111111ull;
-    return x;
-}
-__device__ __forceinline__ uint64_t low_mask(uint32_t b) { return b >= 64 ? ~0ull : ((1ull << b) - 1ull); }
 
-// the exact comparison of an element with the pivot (rare: equal key cells); a free function of values so
-// that the selection state stays in registers
-template <int P, class Src>
-__device__ __attribute__((noinline)) uint32_t classify_exact(Src src, uint32_t ek, uint32_t eid, uint32_t pk, uint32_t pid,
-                                                            double med) {
-    auto val = [&](uint32_t k, uint32_t id) {
-        if (k == kKeyInvisible) return kDblMax;
-        const double r = (k & 1u) ? src.r(id) : key_r(k);
-        return P == 0 ? r : fabs(r - med);
-    };
-    const double v = val(ek, eid), p = val(pk, pid);
+// ---- values and comparisons (P: 0 = the residual, 1 = |residual - med|)
+__device__ __forceinline__ void d_interval(uint32_t k, double med, double& lo, double& hi) {  // |r - med| over the key's cell
+    const double rl = key_r(k), rh = (k & 1u) ? rl + kKeyStep : rl;
+    if (rh <= med) { lo = med - rh; hi = med - rl; }
+    else if (rl >= med) { lo = rl - med; hi = rh - med; }
+    else { lo = 0.0; hi = fmax(med - rl, rh - med); }
+}
+template <class Src>
+__device__ __forceinline__ double value(const Src* src, int P, double med, El e) {  // the reference's vector entry
+    if (e.key == kKeyInvisible) return kDblMax;
+    const double r = (e.key & 1u) ? src->r(e.id) : key_r(e.key);
+    return P == 0 ? r : fabs(r - med);
+}
+// value(a) < value(b), exact (the keys decide almost always; the images only inside one key cell)
+template <class Src>
+__device__ __attribute__((noinline)) bool less_slow(const Src* src, int P, double med, El a, El b) {
+    return value(src, P, med, a) < value(src, P, med, b);
+}
+template <class Src>
+__device__ __forceinline__ bool less(const Src* src, int P, double med, El a, El b) {
+    if (P == 0) {
+        if (a.key != b.key) return a.key < b.key;
+        if (a.key == kKeyInvisible || !(a.key & 1u)) return false;
+    } else {
+        if (a.key == kKeyInvisible) return false;
+        if (b.key == kKeyInvisible) return true;
+        double alo, ahi, blo, bhi;
+        d_interval(a.key, med, alo, ahi);
+        d_interval(b.key, med, blo, bhi);
+        if (ahi < blo) return true;
+        if (alo >= bhi) return false;
+    }
+    return less_slow(src, P, med, a, b);
+}
+// (ge, le) of an element whose key missed the fast tests: the cell's interval, then the exact values
+template <class Src>
+__device__ __attribute__((noinline)) uint32_t classify_slow(const Src* src, int P, double med, uint32_t k, uint32_t id,
+                                                           El pe, double plo, double phi, uint64_t* counter) {
+    if (P == 1) {
+        double lo, hi;
+        d_interval(k, med, lo, hi);
+        if (hi < plo) return 2u;
+        if (lo > phi) return 1u;
+    }
+    atomicAdd((unsigned long long*)counter, 1ull);  // diagnostics
+    const double v = value(src, P, med, El{k, id}), p = value(src, P, med, pe);
     return (!(v < p) ? 1u : 0u) | (!(p < v) ? 2u : 0u);
+}
+
+// ---- heap select (depth limit), one lane: stl_heap.h __adjust_heap / __push_heap / __make_heap /
+// __pop_heap and stl_algo.h __heap_select restated over positions first + i, then the swap of first and
+// nth (tests/cpp/introselect_model.cpp checks the restatement).  Only adversarial inputs reach it; a free
+// function of plain values, so that the selection state never needs an address.
+template <class Src, typename Id>
+struct HeapView {
+    const Src* src;
+    RefShared<Id>* sh;
+    uint32_t* gkey;
+    uint32_t* gid;
+    uint32_t first, base;
+    int where, P;
+    double med;
+    __device__ El get(uint32_t i) const {
+        const uint32_t p = first + i;
+        if (where == kLds) return El{sh->key[p - base], (uint32_t)sh->id[p - base]};
+        if (where == kGlb) return El{gkey[p], gid[p]};
+        return El{src->key(p), p};
+    }
+    __device__ void put(uint32_t i, El e) const {
+        const uint32_t p = first + i;
+        if (where == kLds) { sh->key[p - base] = e.key; sh->id[p - base] = (Id)e.id; }
+        else if (where == kGlb) { gkey[p] = e.key; gid[p] = e.id; }
+    }
+    __device__ bool lt(El a, El b) const { return less(src, P, med, a, b); }
+};
+template <class Src, typename Id>
+__device__ __attribute__((noinline)) void heap_select_fn(HeapView<Src, Id> h, uint32_t middle, uint32_t len, uint32_t nth_rel) {
+    auto push_heap = [&](uint32_t hole, uint32_t top, El value) {
+        uint32_t parent = (hole - 1) / 2;
+        while (hole > top && h.lt(h.get(parent), value)) {
+            h.put(hole, h.get(parent));
+            hole = parent;
+            parent = (hole - 1) / 2;
+        }
+        h.put(hole, value);
+    };
+    auto adjust_heap = [&](uint32_t hole, uint32_t n, El value) {
+        const uint32_t top = hole;
+        uint32_t second = hole;
+        while (n >= 1 && second < (n - 1) / 2) {
+            second = 2 * (second + 1);
+            if (h.lt(h.get(second), h.get(second - 1))) second--;
+            h.put(hole, h.get(second));
+            hole = second;
+        }
+        if ((n & 1u) == 0 && second == (n - 2) / 2) {
+            second = 2 * (second + 1);
+            h.put(hole, h.get(second - 1));
+            hole = second - 1;
+        }
+        push_heap(hole, top, value);
+    };
+    if (middle >= 2) {
+        uint32_t parent = (middle - 2) / 2;
+        while (true) {
+            adjust_heap(parent, middle, h.get(parent));
+            if (parent == 0) break;
+            parent--;
+        }
+    }
+    for (uint32_t i = middle; i < len; ++i)
+        if (h.lt(h.get(i), h.get(0))) {
+            const El v = h.get(i);
+            h.put(i, h.get(0));
+            adjust_heap(0, middle, v);
+        }
+    const El f0 = h.get(0), n0 = h.get(nth_rel);  // std::iter_swap(first, nth)
+    h.put(0, n0);
+    h.put(nth_rel, f0);
 }
 
 template <class Src, typename Id>
 struct RefSel {
     using Shared = RefShared<Id>;
     static constexpr int kCap = Shared::kCap;
-    Src src;
+    static constexpr int R = sizeof(Id) == 2 ? 2 : 16;  // step records per lane (segments up to 64 R steps / wave)
+    const Src* src;   // the source, kept in LDS (the slow paths take this pointer, never a copy)
     Shared& sh;
+    typename Src::KeyBase kb;  // round-1 keys (inline path)
     uint32_t* gkey;   // pair's global segment keys / ids (absolute positions)
     uint32_t* gid;
     uint32_t* glp;    // swap partners L_k / R_k of the global and copy rounds
     uint32_t* grp;
-    uint64_t* gmge;   // step records of segments past kMeta steps
+    uint64_t* gmge;   // step records of segments past kMeta steps (R > 1)
     uint64_t* gmle;
-    uint32_t* ggpre;
-    uint32_t* glsuf;
     uint32_t M, nth;
-    double med;       // pass 1
     int tid, lane, wave;
+    int P;            // the pass: 0 median, 1 MAD
+    double med;       // pass 1
     // block-uniform state
     uint32_t first, last, base;
     int where, depth, rec;
     El lo_el;
     Pivot pv;
 
-    // ---------------------------------------------------------------- values and comparisons
-    template <int P>
-    __device__ __forceinline__ double value(El e) const {  // the reference's vector entry (exact)
-        if (e.key == kKeyInvisible) return kDblMax;
-        const double r = (e.key & 1u) ? src.r(e.id) : key_r(e.key);
-        return P == 0 ? r : fabs(r - med);
+    // ---------------------------------------------------------------- storage (runtime `where`)
+    __device__ __forceinline__ El get(uint32_t p) const {
+        if (where == kLds) return El{sh.key[p - base], (uint32_t)sh.id[p - base]};
+        if (where == kGlb) return El{gkey[p], gid[p]};
+        return El{Src::key_at(kb, p), p};
     }
-    __device__ __forceinline__ void d_interval(uint32_t k, double& lo, double& hi) const {  // |r - med| over the key's cell
-        const double rl = key_r(k), rh = (k & 1u) ? rl + kKeyStep : rl;
-        if (rh <= med) { lo = med - rh; hi = med - rl; }
-        else if (rl >= med) { lo = rl - med; hi = rh - med; }
-        else { lo = 0.0; hi = fmax(med - rl, rh - med); }
+    __device__ __forceinline__ void put(uint32_t p, El e) {
+        if (where == kLds) { sh.key[p - base] = e.key; sh.id[p - base] = (Id)e.id; }
+        else if (where == kGlb) { gkey[p] = e.key; gid[p] = e.id; }
     }
-    template <int P>
-    __device__ __forceinline__ bool less(El a, El b) const {  // value(a) < value(b)
-        if (P == 0) {
-            if (a.key != b.key) return a.key < b.key;
-            if (a.key == kKeyInvisible || !(a.key & 1u)) return false;
-            return value<0>(a) < value<0>(b);
-        } else {
-            if (a.key == kKeyInvisible) return false;
-            if (b.key == kKeyInvisible) return true;
-            double alo, ahi, blo, bhi;
-            d_interval(a.key, alo, ahi);
-            d_interval(b.key, blo, bhi);
-            if (ahi < blo) return true;
-            if (alo >= bhi) return false;
-            return value<1>(a) < value<1>(b);
-        }
+    // the segment after the median-of-three swap (first <-> ch), before it is stored
+    __device__ __forceinline__ El elp(uint32_t p) const {
+        if (p == first) return pv.e;
+        if (p == pv.ch) return pv.f0;
+        return get(p);
     }
+    __device__ __forceinline__ uint32_t idp(uint32_t p) const { return elp(p).id; }
+
     // (ge, le) = (!(a < p), !(p < a)) as bits 0, 1 for the element of key k at position p
-    template <int P, int W>
     __device__ __forceinline__ uint32_t classify(uint32_t k, uint32_t p) const {
         if (P == 0) {
             if (k != pv.e.key) return k < pv.e.key ? 2u : 1u;
@@ -207,370 +309,459 @@ struct RefSel {
             if (g >= pv.kA + 2 && g <= pv.kB - 2) return 2u;
             // |r - med| > phi for the whole cell: r two grid steps outside [med - phi, med + phi]
             if (g <= pv.kC - 2 || g >= pv.kD + 2) return 1u;
-            double lo, hi;
-            d_interval(k, lo, hi);
-            if (hi < pv.plo) return 2u;
-            if (lo > pv.phi) return 1u;
         }
-        return classify_exact<P, Src>(src, k, elp<W>(p).id, pv.e.key, pv.e.id, med);
+        return classify_slow(src, P, med, k, idp(p), pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
     }
-    template <int P>
-    __device__ __forceinline__ void pivot_info() {  // the pass-1 interval and thresholds of pv.e
-        pv.inv = pv.e.key == kKeyInvisible;
-        if (P == 1 && !pv.inv) {
-            d_interval(pv.e.key, pv.plo, pv.phi);
+    // the pivot: std::__move_median_to_first(first, first + 1, first + S/2, last - 1) and the pass-1
+    // interval / thresholds of the chosen element (uniform; every caller lane computes the same)
+    __device__ __forceinline__ void choose_pivot() {
+        const uint32_t S = last - first, A = first + 1, B = first + S / 2, C = last - 1;
+        const El a = get(A), b = get(B), c = get(C);
+        uint32_t ch;
+        El e;
+        if (less(src, P, med, a, b)) {
+            if (less(src, P, med, b, c)) { ch = B; e = b; }
+            else if (less(src, P, med, a, c)) { ch = C; e = c; }
+            else { ch = A; e = a; }
+        } else if (less(src, P, med, a, c)) { ch = A; e = a; }
+        else if (less(src, P, med, b, c)) { ch = C; e = c; }
+        else { ch = B; e = b; }
+        pv.e = e;
+        pv.f0 = get(first);
+        pv.ch = ch;
+        pv.inv = e.key == kKeyInvisible;
+        pv.plo = pv.phi = 0.0;
+        pv.kA = pv.kB = pv.kC = pv.kD = 0;
+        // pass 1, as key ranges: visible keys are > 2^29 (|r| <= 255), so tC = 0 / tD = ~0 are empty ranges
+        pv.tA = 1; pv.tB = 0; pv.tC = 0; pv.tD = kKeyInvisible;
+        pv.inv_c = 1u;  // an invisible slot is DBL_MAX: greater than a visible pivot
+        if (P == 1 && pv.inv) {
+            pv.tA = 0; pv.tB = kKeyInvisible - 1; pv.inv_c = 3u;  // every visible slot is less; DBL_MAX equal
+        } else if (P == 1) {
+            d_interval(e.key, med, pv.plo, pv.phi);
             pv.kA = key_grid(med - pv.plo);
             pv.kB = key_grid(med + pv.plo);
             pv.kC = key_grid(med - pv.phi);
             pv.kD = key_grid(med + pv.phi);
+            const int64_t a0 = 2 * (pv.kA + 2), b0 = 2 * (pv.kB - 2) + 1, c0 = 2 * (pv.kC - 2) + 1, d0 = 2 * (pv.kD + 2);
+            if (a0 <= b0 && b0 >= 0 && a0 <= (int64_t)kKeyInvisible - 1) {
+                pv.tA = (uint32_t)(a0 < 0 ? 0 : a0);
+                pv.tB = (uint32_t)(b0 > (int64_t)kKeyInvisible - 1 ? (int64_t)kKeyInvisible - 1 : b0);
+            }
+            if (c0 >= 0) pv.tC = (uint32_t)(c0 > (int64_t)kKeyInvisible - 1 ? (int64_t)kKeyInvisible - 1 : c0);
+            if (d0 <= (int64_t)kKeyInvisible - 1) pv.tD = (uint32_t)(d0 < 0 ? 0 : d0);
         }
     }
+    // the class of key k without branches: slow = the keys cannot decide (same cell as the pivot's)
+    template <int PP>
+    __device__ __forceinline__ uint32_t fast_cls(uint32_t k, bool& slow) const {
+        if (PP == 0) {
+            const bool lt = k < pv.e.key, gt = k > pv.e.key;
+            slow = !lt && !gt && k != kKeyInvisible && (k & 1u);
+            return lt ? 2u : (gt ? 1u : 3u);
+        } else {
+            const bool inv = k == kKeyInvisible;
+            const bool ls = k >= pv.tA && k <= pv.tB, gr = k <= pv.tC || k >= pv.tD;
+            slow = !inv && !ls && !gr;
+            return inv ? pv.inv_c : (ls ? 2u : (gr ? 1u : 0u));
+        }
+    }
+    // sweep of steps [s0, s0 + n): step s's GE / LE ballots to mge[s] / mle[s] (lane 0 stores).  The loads
+    // of 8 steps are issued before any is used; the classification is branch-free, the rare key-cell ties
+    // go to classify_slow under one wave-uniform test.
+    template <int W, int PP>
+    __device__ __forceinline__ void sweep_p(uint32_t b0, uint32_t s0, uint32_t n, uint64_t* mge, uint64_t* mle) {
+        for (uint32_t j0 = 0; j0 < n; j0 += 8) {
+            uint32_t kv[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint32_t p = b0 + 64 * (s0 + j0 + (uint32_t)b) + (uint32_t)lane;
+                uint32_t k = 0;
+                if (j0 + (uint32_t)b < n && p < last) {
+                    if (W == kLds) k = sh.key[p - base];
+                    else if (W == kGlb) k = gkey[p];
+                    else k = Src::key_at(kb, p);
+                }
+                kv[b] = k;
+            }
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const uint32_t j = j0 + (uint32_t)b;
+                if (j >= n) break;  // wave-uniform
+                const uint32_t q = b0 + 64 * (s0 + j) + (uint32_t)lane;
+                const uint32_t k = q == pv.ch ? pv.f0.key : kv[b];
+                bool slow;
+                uint32_t c = fast_cls<PP>(k, slow);
+                const bool in = q > first && q < last;  // position first holds the pivot: LE only
+                c = in ? c : (q == first ? 2u : 0u);
+                slow = slow && in;
+                if (__ballot(slow)) {
+                    if (slow) c = classify_slow(src, P, med, k, elp(q).id, pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
+                }
+                const uint64_t bg = __ballot(c & 1u), bl = __ballot(c & 2u);
+                if (lane == 0) { mge[s0 + j] = bg; mle[s0 + j] = bl; }
+            }
+        }
+    }
+    template <int W>
+    __device__ __forceinline__ void sweep(uint32_t b0, uint32_t s0, uint32_t n, uint64_t* mge, uint64_t* mle) {
+        if (P == 0) sweep_p<W, 0>(b0, s0, n, mge, mle);
+        else sweep_p<W, 1>(b0, s0, n, mge, mle);
+    }
 
-    // ---------------------------------------------------------------- storage
-    template <int W>
-    __device__ __forceinline__ El get(uint32_t p) const {
-        if (W == kSrc) return El{src.key(p), p};
-        if (W == kGlb) return El{gkey[p], gid[p]};
-        return El{sh.key[p - base], (uint32_t)sh.id[p - base]};
-    }
-    template <int W>
-    __device__ __forceinline__ uint4 get4(uint32_t p) const {  // keys p .. p+3 (p a multiple of 4)
-        if (W == kSrc) return src.key4(p);
-        if (W == kGlb) return *reinterpret_cast<const uint4*>(gkey + p);
-        return *reinterpret_cast<const uint4*>(&sh.key[p - base]);
-    }
-    template <int W>
-    __device__ __forceinline__ void put(uint32_t p, El e) {
-        if (W == kGlb) { gkey[p] = e.key; gid[p] = e.id; }
-        if (W == kLds) { sh.key[p - base] = e.key; sh.id[p - base] = (Id)e.id; }
-    }
-    // the segment after the median-of-three swap (first <-> ch), before it is stored
-    template <int W>
-    __device__ __forceinline__ El elp(uint32_t p) const {
-        if (p == first) return pv.e;
-        if (p == pv.ch) return pv.f0;
-        return get<W>(p);
-    }
-    __device__ __forceinline__ El get_any(uint32_t p) const {
-        if (where == kGlb) return get<kGlb>(p);
-        if (where == kLds) return get<kLds>(p);
-        return get<kSrc>(p);
-    }
-    __device__ __forceinline__ void put_any(uint32_t p, El e) {
-        if (where == kGlb) put<kGlb>(p, e);
-        else if (where == kLds) put<kLds>(p, e);
-    }
-
-    // ---------------------------------------------------------------- one partition round
-    // Steps are 64 positions from b0 = first & ~63.  The classification sweep stores each step's GE / LE
-    // ballots (16-B loads: a wave covers 256 positions, the four 64-lane ballots interleave into four
-    // step records); the scans, the crossing, L_{Ks+1} / R_{Ks} and the swaps work from those records.
-    // kLM: the step records live in LDS (segments up to kMeta steps) or in the global scratch.
-    template <int P, int W, bool kLM>
+    // ---------------------------------------------------------------- one block round (large segments)
+    // Steps are 64 positions from b0 = first & ~63; wave w owns the steps [w spw, (w + 1) spw) with
+    // spw = ceil(steps / 16) <= 64 R, lane l holding steps w spw + 64 r + l in registers: GE / LE ballots,
+    // in-wave prefix sums, the GE count before and the LE count from each step.  Wave 0 chooses the pivot
+    // and finds the crossing; barriers after the pivot, the sweep, the crossing, the partner lists and the
+    // swaps.
     __device__ __forceinline__ void round() {
-        const uint32_t S = last - first, b0 = first & ~63u, ns = (last - b0 + 63) / 64, ng = (ns + 3) / 4;
-        uint64_t* const mge = kLM ? sh.mge : gmge;
-        uint64_t* const mle = kLM ? sh.mle : gmle;
-        uint32_t* const gpre = kLM ? sh.gpre : ggpre;
-        uint32_t* const lsuf = kLM ? sh.lsuf : glsuf;
+        const uint32_t b0 = first & ~63u, ns = (last - b0 + 63) / 64;
+        const uint32_t spw = (ns + kRW - 1) / kRW;
+        uint64_t* const mge = R <= 2 ? sh.mge : gmge;
+        uint64_t* const mle = R <= 2 ? sh.mle : gmle;
         uint64_t tp = clock64();
         auto phase = [&](int i) {
-            if (tid == 0) { const uint64_t t = clock64(); sh.stamp[8 + 6 * W + i] += t - tp; tp = t; }
+            if (tid == 0) { const uint64_t t = clock64(); sh.stamp[8 + 5 * where + i] += t - tp; tp = t; }
         };
-        // ---- pivot: std::__move_median_to_first(first, first + 1, first + S/2, last - 1), computed by
-        // every thread (same reads, same answer; no broadcast)
-        {
-            const uint32_t A = first + 1, B = first + S / 2, C = last - 1;
-            const El a = get<W>(A), b = get<W>(B), c = get<W>(C);
-            uint32_t ch;
-            El e;
-            if (less<P>(a, b)) {
-                if (less<P>(b, c)) { ch = B; e = b; }
-                else if (less<P>(a, c)) { ch = C; e = c; }
-                else { ch = A; e = a; }
-            } else if (less<P>(a, c)) { ch = A; e = a; }
-            else if (less<P>(b, c)) { ch = C; e = c; }
-            else { ch = B; e = b; }
-            pv.e = e;
-            pv.f0 = get<W>(first);
-            pv.ch = ch;
-            pivot_info<P>();
+        if (wave == 0) {
+            choose_pivot();
+            if (lane == 0) {
+                sh.piv = pv;
+                sh.cut_l = kNone; sh.cut_r = kNone; sh.l_ks = kNone;
+            }
         }
+        __syncthreads();
+        pv = sh.piv;
         phase(0);
-        // ---- classification sweep
-        for (uint32_t g0 = (uint32_t)wave; g0 < ng; g0 += kRW * kBatch) {
-            uint4 kv[kBatch];
+        // ---- classification sweep of the wave's steps
+        const uint32_t ws0 = (uint32_t)wave * spw;
+        const uint32_t wsn = ws0 >= ns ? 0u : (ns - ws0 < spw ? ns - ws0 : spw);
+        if (where == kLds) sweep<kLds>(b0, ws0, wsn, mge, mle);
+        else if (where == kGlb) sweep<kGlb>(b0, ws0, wsn, mge, mle);
+        else sweep<kSrc>(b0, ws0, wsn, mge, mle);
+        if (R > 2) __threadfence_block();  // global step records: lane 0's stores before the lanes' loads
+        uint64_t mg[R], ml[R];
+        uint32_t gex[R], lex[R], gw = 0, lw = 0;
 #pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                const uint32_t g = g0 + (uint32_t)(kRW * b), p = b0 + 256 * g + 4 * (uint32_t)lane;
-                kv[b] = (g < ng && p < last) ? get4<W>(p) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                const uint32_t g = g0 + (uint32_t)(kRW * b), p = b0 + 256 * g + 4 * (uint32_t)lane;
-                if (g >= ng) break;  // wave-uniform
-                const uint32_t kk[4] = {kv[b].x, kv[b].y, kv[b].z, kv[b].w};
-                uint64_t bg[4], bl[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t q = p + (uint32_t)j;
-                    uint32_t c = 0;
-                    if (q >= first && q < last) {
-                        if (q == first) c = 2u;  // the pivot: the right scan's sentinel, outside the left scan
-                        else c = classify<P, W>(q == pv.ch ? pv.f0.key : kk[j], q);
-                    }
-                    bg[j] = __ballot(c & 1u);
-                    bl[j] = __ballot(c & 2u);
-                }
-                if (lane < 4) {  // lane q writes step 4 g + q: positions 64 q + 4 l + j hold lane 16 q + l, key j
-                    const uint32_t s = 4 * g + (uint32_t)lane;
-                    if (s < ns) {
-                        uint64_t mg = 0, ml = 0;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            mg |= spread4(bg[j] >> (16 * lane)) << j;
-                            ml |= spread4(bl[j] >> (16 * lane)) << j;
-                        }
-                        mge[s] = mg;
-                        mle[s] = ml;
-                    }
-                }
-            }
+        for (int r = 0; r < R; ++r) {
+            const uint32_t j = 64 * (uint32_t)r + (uint32_t)lane;
+            mg[r] = j < wsn ? mge[ws0 + j] : 0ull;
+            ml[r] = j < wsn ? mle[ws0 + j] : 0ull;
+            const uint32_t cg = (uint32_t)__popcll(mg[r]), cl = (uint32_t)__popcll(ml[r]);
+            const uint32_t gi = wave_incl_scan(cg), li = wave_incl_scan(cl);
+            gex[r] = gw + gi - cg;
+            lex[r] = lw + li - cl;
+            gw += lane_read(gi, 63);
+            lw += lane_read(li, 63);
         }
+        if (lane == 0) { sh.wsum[wave][0] = gw; sh.wsum[wave][1] = lw; }
         __syncthreads();
         phase(1);
-        // ---- scans over the steps: thread t owns steps [t * per, (t + 1) * per)
-        const uint32_t per = (ns + kRT - 1) / kRT, s_lo = (uint32_t)tid * per;
-        const uint32_t s_hi = s_lo + per < ns ? s_lo + per : ns;
-        uint32_t gs = 0, ls = 0;
-        for (uint32_t s = s_lo; s < s_hi; ++s) { gs += (uint32_t)__popcll(mge[s]); ls += (uint32_t)__popcll(mle[s]); }
-        const uint32_t gi = wave_incl_scan(gs), li = wave_incl_scan(ls);
-        if (lane == 63) { sh.wsum[wave][0] = gi; sh.wsum[wave][1] = li; }
+        // ---- wave prefixes (lane i < 16 holds wave i's totals); the crossing t* (first split with G >= Lc):
+        // its wave, its step, its bit, Ks = max(G(t*-1), Lc(t*)), found by wave 0
+        const uint32_t wg = lane < kRW ? sh.wsum[lane][0] : 0u, wl = lane < kRW ? sh.wsum[lane][1] : 0u;
+        const uint32_t wgi = wave_incl_scan(wg), wli = wave_incl_scan(wl);
+        const uint32_t lt = lane_read(wli, 63);
+        const uint32_t gb = lane_read(wgi - wg, wave), lb = lane_read(wli - wl, wave);
+        if (wave == 0) {
+            const uint32_t g_start = wgi - wg, l_start = lt - (wli - wl);
+            const uint32_t wc = (uint32_t)__builtin_ctzll(__ballot(lane < kRW && g_start < l_start && g_start + wg >= l_start - wl));
+            const uint32_t cs0 = wc * spw, csn = cs0 >= ns ? 0u : (ns - cs0 < spw ? ns - cs0 : spw);
+            uint32_t gcar = lane_read(g_start, (int)wc), lcar = lane_read(l_start, (int)wc), sc = kNone;
+            for (uint32_t j0 = 0; j0 < csn && sc == kNone; j0 += 64) {
+                const uint32_t j = j0 + (uint32_t)lane;
+                const uint64_t a = j < csn ? mge[cs0 + j] : 0ull, bb = j < csn ? mle[cs0 + j] : 0ull;
+                const uint32_t cg = (uint32_t)__popcll(a), cl = (uint32_t)__popcll(bb);
+                const uint32_t gi = wave_incl_scan(cg), li = wave_incl_scan(cl);
+                const uint32_t gs = gcar + gi - cg, ls = lcar - (li - cl);
+                const uint64_t hit = __ballot(j < csn && gs < ls && gs + cg >= ls - cl);
+                if (hit) {
+                    const int L = __builtin_ctzll(hit);
+                    sc = cs0 + j0 + (uint32_t)L;
+                    gcar = lane_read(gs, L);
+                    lcar = lane_read(ls, L);
+                } else {
+                    gcar += lane_read(gi, 63);
+                    lcar -= lane_read(li, 63);
+                }
+            }
+            const uint64_t a = mge[sc], bb = mle[sc];
+            uint32_t lo = 1, hi = 64;  // smallest b with G(b) >= Lc(b) inside step sc
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) / 2;
+                const uint64_t lm = low_mask(m);
+                if (gcar + (uint32_t)__popcll(a & lm) >= lcar - (uint32_t)__popcll(bb & lm)) hi = m;
+                else lo = m + 1;
+            }
+            const uint32_t g1 = gcar + (uint32_t)__popcll(a & low_mask(lo - 1));
+            const uint32_t l2 = lcar - (uint32_t)__popcll(bb & low_mask(lo));
+            if (lane == 0) sh.ks = g1 > l2 ? g1 : l2;
+        }
         __syncthreads();
         phase(2);
-        uint32_t gb = 0, lb = 0, lt = 0;
-        for (int w = 0; w < kRW; ++w) {
-            const uint32_t wg = sh.wsum[w][0], wl = sh.wsum[w][1];
-            gb += w < wave ? wg : 0u;
-            lb += w < wave ? wl : 0u;
-            lt += wl;
-        }
-        // ---- per step G, Lc at its start; Ks = max_t min(G(t), Lc(t)): with t* the first split where
-        // G >= Lc (G rises, Lc falls), Ks = max(G(t* - 1), Lc(t*)); the step holding t* finds it
-        {
-            uint32_t gex = gb + gi - gs, lfrom = lt - (lb + li - ls);
-            for (uint32_t s = s_lo; s < s_hi; ++s) {
-                const uint64_t mg = mge[s], ml = mle[s];
-                gpre[s] = gex;
-                lsuf[s] = lfrom;
-                const uint32_t cg = (uint32_t)__popcll(mg), cl = (uint32_t)__popcll(ml);
-                if (gex < lfrom && gex + cg >= lfrom - cl) {
-                    uint32_t lo = 1, hi = 64;  // smallest b with G(b) >= Lc(b)
-                    while (lo < hi) {
-                        const uint32_t m = (lo + hi) / 2;
-                        const uint64_t lm = low_mask(m);
-                        if (gex + (uint32_t)__popcll(mg & lm) >= lfrom - (uint32_t)__popcll(ml & lm)) hi = m;
-                        else lo = m + 1;
-                    }
-                    const uint32_t g1 = gex + (uint32_t)__popcll(mg & low_mask(lo - 1));
-                    const uint32_t l2 = lfrom - (uint32_t)__popcll(ml & low_mask(lo));
-                    sh.ks = g1 > l2 ? g1 : l2;
+        const uint32_t ks = sh.ks;
+        uint32_t gpre[R], lsuf[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) { gpre[r] = gb + gex[r]; lsuf[r] = lt - lb - lex[r]; }
+        // ---- the swap partners: each lane walks the set bits of its own steps.  L_k (GE rank k <= Ks) and
+        // R_k (LE rank k from the right) to the lists; L_{Ks+1}, L_{Ks}, R_{Ks} to shared scalars
+        const bool lds_lists = where == kLds;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t j = 64 * (uint32_t)r + (uint32_t)lane;
+            if (j >= wsn) continue;
+            const uint32_t sb = b0 + 64 * (ws0 + j);  // the step's first position
+            uint64_t a = mg[r];
+            uint32_t k = gpre[r] + 1;  // GE ranks, ascending with the bit
+            while (a != 0 && k <= ks + 1) {
+                const uint32_t pos = sb + (uint32_t)__builtin_ctzll(a);
+                a &= a - 1;
+                if (k <= ks) {
+                    if (lds_lists) sh.lp[k - 1] = (uint16_t)(pos - b0);
+                    else glp[k - 1] = pos;
                 }
-                gex += cg;
-                lfrom -= cl;
+                if (k == ks + 1) sh.cut_l = pos;
+                if (k == ks) sh.l_ks = pos;
+                ++k;
+            }
+            uint64_t bb = ml[r];
+            k = lsuf[r] - (uint32_t)__popcll(bb) + 1;  // LE right-ranks, ascending downwards from the top bit
+            while (bb != 0 && k <= ks) {
+                const uint32_t hb = 63u - (uint32_t)__builtin_clzll(bb);
+                const uint32_t pos = sb + hb;
+                bb &= ~(1ull << hb);
+                if (lds_lists) sh.rp[k - 1] = (uint16_t)(pos - b0);
+                else grp[k - 1] = pos;
+                if (k == ks) sh.cut_r = pos;
+                ++k;
             }
         }
-        if (tid == 0) { sh.cut_l = kNone; sh.cut_r = kNone; sh.l_ks = kNone; }
         __syncthreads();
         phase(3);
-        const uint32_t ks = sh.ks;
-        // ---- the swap partners: a wave takes a step, a lane a bit.  L_k (GE rank k <= Ks) and R_k (LE rank
-        // k from the right) go to the lists lp / rp; L_{Ks+1}, L_{Ks} and R_{Ks} to shared scalars
-        {
-            uint16_t* const lp16 = sh.lp;
-            uint16_t* const rp16 = sh.rp;
-            for (uint32_t s = (uint32_t)wave; s < ns; s += kRW) {
-                const uint64_t mg = mge[s], ml = mle[s];
-                const uint32_t g0 = gpre[s], l0 = lsuf[s];
-                const uint64_t below = low_mask((uint32_t)lane);
-                const uint32_t pos = b0 + 64 * s + (uint32_t)lane;
-                if (g0 < ks + 1 && ((mg >> lane) & 1ull)) {
-                    const uint32_t k = g0 + (uint32_t)__popcll(mg & below) + 1;
-                    if (k <= ks) {
-                        if (W == kLds) lp16[k - 1] = (uint16_t)(pos - b0);
-                        else glp[k - 1] = pos;
-                    }
-                    if (k == ks + 1) sh.cut_l = pos;
-                    if (k == ks) sh.l_ks = pos;
+        const uint32_t cut_l = sh.cut_l, cut_r = ks > 0 ? sh.cut_r : kNone;
+        const uint32_t cut = cut_l < cut_r ? cut_l : cut_r;
+        const bool right = cut <= nth;  // the side introselect continues with
+        const uint32_t nf = right ? cut : first, nl = right ? last : cut;
+        auto lpos = [&](uint32_t k) { return lds_lists ? b0 + sh.lp[k] : glp[k]; };  // L_{k+1}
+        auto rpos = [&](uint32_t k) { return lds_lists ? b0 + sh.rp[k] : grp[k]; };  // R_{k+1}
+        // ---- vec[nth - 1] after this partition, if this cut leaves it behind for good
+        if (cut == nth && !rec) {
+            lo_el = (ks > 0 && sh.l_ks == cut - 1) ? elp(cut_r) : elp(cut - 1);
+            __syncthreads();  // read before any swap (block-uniform branch)
+        }
+        if (where == kSrc) {
+            // ---- copy the surviving side out of the read-only keys (coalesced), then the swap targets take
+            // their partners
+            uint32_t nb = nf & ~63u;
+            const int dst = (nl - nb) <= (uint32_t)kCap && M <= (sizeof(Id) == 2 ? 65536u : 0xFFFFFFFFu) ? kLds : kGlb;
+            if (dst == kGlb) nb = 0;
+            const uint32_t n = nl - nf;
+            for (uint32_t i0 = (uint32_t)tid; i0 < n; i0 += kRT * 8) {
+                uint32_t kk[8];
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    const uint32_t i = i0 + (uint32_t)(kRT * b);
+                    kk[b] = i < n ? Src::key_at(kb, nf + i) : 0u;
                 }
-                if (l0 - (uint32_t)__popcll(ml) < ks && ((ml >> lane) & 1ull)) {
-                    const uint32_t k = l0 - (uint32_t)__popcll(ml & below);
-                    if (k <= ks) {
-                        if (W == kLds) rp16[k - 1] = (uint16_t)(pos - b0);
-                        else grp[k - 1] = pos;
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    const uint32_t i = i0 + (uint32_t)(kRT * b), p = nf + i;
+                    if (i >= n) break;
+                    const El e = p == first ? pv.e : (p == pv.ch ? pv.f0 : El{kk[b], p});
+                    if (dst == kLds) { sh.key[p - nb] = e.key; sh.id[p - nb] = (Id)e.id; }
+                    else { gkey[p] = e.key; gid[p] = e.id; }
+                }
+            }
+            __syncthreads();
+            for (uint32_t k0 = (uint32_t)tid; k0 < ks; k0 += kRT * kBatch) {
+                uint32_t to[kBatch];
+                El ev[kBatch];
+#pragma unroll
+                for (int b = 0; b < kBatch; ++b) {
+                    const uint32_t k = k0 + (uint32_t)(kRT * b);
+                    if (k < ks) {
+                        const uint32_t lq = lpos(k), rq = rpos(k);
+                        to[b] = right ? rq : lq;
+                        ev[b] = elp(right ? lq : rq);
                     }
-                    if (k == ks) sh.cut_r = pos;
+                }
+#pragma unroll
+                for (int b = 0; b < kBatch; ++b) {
+                    if (k0 + (uint32_t)(kRT * b) >= ks) break;
+                    if (dst == kLds) { sh.key[to[b] - nb] = ev[b].key; sh.id[to[b] - nb] = (Id)ev[b].id; }
+                    else { gkey[to[b]] = ev[b].key; gid[to[b]] = ev[b].id; }
+                }
+            }
+            where = dst;
+            base = nb;
+        } else {
+            // ---- in place, on the surviving side only: R_k <- old L_k (right) or L_k <- old R_k (left).
+            // Reads (one side) and writes (the other) are disjoint; the two positions of the median-of-three
+            // swap are read from pv (registers) and written by thread 0 unless a swap target
+            for (uint32_t k0 = (uint32_t)tid; k0 < ks; k0 += kRT * kBatch) {
+                uint32_t to[kBatch];
+                El ev[kBatch];
+#pragma unroll
+                for (int b = 0; b < kBatch; ++b) {
+                    const uint32_t k = k0 + (uint32_t)(kRT * b);
+                    if (k < ks) {
+                        const uint32_t lq = lpos(k), rq = rpos(k);
+                        to[b] = right ? rq : lq;
+                        ev[b] = elp(right ? lq : rq);
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b < kBatch; ++b)
+                    if (k0 + (uint32_t)(kRT * b) < ks) put(to[b], ev[b]);
+            }
+            if (tid == 0) {
+                if (first >= nf && first < nl) put(first, pv.e);
+                if (pv.ch >= nf && pv.ch < nl) {  // is ch a swap target? its ranks from the step records
+                    const uint32_t s = (pv.ch - b0) / 64, bit = (pv.ch - b0) % 64;
+                    const uint64_t below = low_mask(bit), a = mge[s], bb = mle[s];
+                    const uint32_t ow = s / spw;
+                    uint32_t g0 = lane_read(wgi - wg, (int)ow), l0 = lt - lane_read(wli - wl, (int)ow);
+                    for (uint32_t t = ow * spw; t < s; ++t) { g0 += (uint32_t)__popcll(mge[t]); l0 -= (uint32_t)__popcll(mle[t]); }
+                    bool tgt = false;
+                    if (!right && ((a >> bit) & 1ull)) tgt = g0 + (uint32_t)__popcll(a & below) + 1 <= ks;
+                    if (right && ((bb >> bit) & 1ull)) tgt = l0 - (uint32_t)__popcll(bb & below) <= ks;
+                    if (!tgt) put(pv.ch, pv.f0);
                 }
             }
         }
         __syncthreads();
         phase(4);
-        const uint32_t cut_l = sh.cut_l, cut_r = ks > 0 ? sh.cut_r : kNone;
-        const uint32_t cut = cut_l < cut_r ? cut_l : cut_r;
-        const bool right = cut <= nth;  // the side introselect continues with
-        const uint32_t nf = right ? cut : first, nl = right ? last : cut;
-        // ---- vec[nth - 1] after this partition, if this cut leaves it behind for good
-        if (cut == nth && !rec) {
-            lo_el = (ks > 0 && sh.l_ks == cut - 1) ? elp<W>(cut_r) : elp<W>(cut - 1);
-            __syncthreads();  // read before any swap (block-uniform branch)
-        }
-        int dst = W;
-        uint32_t nb = base;
-        if (W == kSrc) {
-            // ---- copy the surviving side out of the read-only keys (the swap targets follow)
-            nb = nf & ~63u;
-            dst = (nl - nb) <= (uint32_t)kCap && M <= (sizeof(Id) == 2 ? 65536u : 0xFFFFFFFFu) ? kLds : kGlb;
-            if (dst == kGlb) nb = 0;
-            const uint32_t n = nl - nf;
-            for (uint32_t i0 = (uint32_t)tid; i0 < n; i0 += kRT * kBatch) {
-                El ev[kBatch];
-#pragma unroll
-                for (int b = 0; b < kBatch; ++b) {
-                    const uint32_t i = i0 + (uint32_t)(kRT * b);
-                    if (i < n) ev[b] = elp<kSrc>(nf + i);
-                }
-#pragma unroll
-                for (int b = 0; b < kBatch; ++b) {
-                    const uint32_t i = i0 + (uint32_t)(kRT * b);
-                    if (i < n) {
-                        if (dst == kLds) { sh.key[nf + i - nb] = ev[b].key; sh.id[nf + i - nb] = (Id)ev[b].id; }
-                        else { gkey[nf + i] = ev[b].key; gid[nf + i] = ev[b].id; }
-                    }
-                }
-            }
-            __syncthreads();
-        }
-        auto store = [&](uint32_t p, El e) {
-            if (dst == kLds) { sh.key[p - nb] = e.key; sh.id[p - nb] = (Id)e.id; }
-            else { gkey[p] = e.key; gid[p] = e.id; }
-        };
-        // ---- the swaps on the surviving side: R_k <- old L_k (right) or L_k <- old R_k (left), k <= Ks.
-        // Reads (one side) and writes (the other) are disjoint; the two positions of the median-of-three
-        // swap are read from pv (registers)
-        for (uint32_t k0 = (uint32_t)tid; k0 < ks; k0 += kRT * kBatch) {
-            uint32_t to[kBatch];
-            El ev[kBatch];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                const uint32_t k = k0 + (uint32_t)(kRT * b);
-                if (k < ks) {
-                    const uint32_t lq = W == kLds ? b0 + sh.lp[k] : glp[k], rq = W == kLds ? b0 + sh.rp[k] : grp[k];
-                    to[b] = right ? rq : lq;
-                    ev[b] = elp<W>(right ? lq : rq);
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b)
-                if (k0 + (uint32_t)(kRT * b) < ks) store(to[b], ev[b]);
-        }
-        if (W != kSrc && tid == 0) {  // in place: the median-of-three swap, unless its slot is a swap target
-            if (first >= nf && first < nl) store(first, pv.e);
-            if (pv.ch >= nf && pv.ch < nl) {
-                const uint32_t s = (pv.ch - b0) / 64, bit = (pv.ch - b0) % 64;
-                const uint64_t below = low_mask(bit);
-                bool tgt = false;
-                if (!right && ((mge[s] >> bit) & 1ull)) tgt = gpre[s] + (uint32_t)__popcll(mge[s] & below) + 1 <= ks;
-                if (right && ((mle[s] >> bit) & 1ull)) tgt = lsuf[s] - (uint32_t)__popcll(mle[s] & below) <= ks;
-                if (!tgt) store(pv.ch, pv.f0);
-            }
-        }
-        where = dst;
-        base = nb;
-        __syncthreads();
-        phase(5);
         rec = rec || cut == nth;
         first = nf;
         last = nl;
     }
 
-    template <int P, int W>
-    __device__ __forceinline__ void round_any() {
-        const uint32_t ns = (last - (first & ~63u) + 63) / 64;
-        if (W == kLds || ns <= (uint32_t)kMeta) round<P, W, true>();
-        else round<P, W, false>();
-    }
-
-    // ---------------------------------------------------------------- heap select (depth limit), one lane
-    // stl_heap.h __adjust_heap / __push_heap / __make_heap / __pop_heap and stl_algo.h __heap_select,
-    // restated over positions first + i (tests/cpp/introselect_model.cpp checks the restatement)
-    template <int P>
-    __device__ __forceinline__ void push_heap(uint32_t hole, uint32_t top, El value) {
-        uint32_t parent = (hole - 1) / 2;
-        while (hole > top && less<P>(get_any(first + parent), value)) {
-            put_any(first + hole, get_any(first + parent));
-            hole = parent;
-            parent = (hole - 1) / 2;
+    // ---------------------------------------------------------------- one round of a small LDS segment
+    // (<= 64 steps) by one wave, no barriers: lane = step for the records, lane = bit for the partners.
+    // LDS accesses of one wave complete in program order, so a lane reads what another lane wrote in an
+    // earlier instruction.
+    __device__ __forceinline__ void wave_round() {
+        const uint32_t b0 = first & ~63u, ns = (last - b0 + 63) / 64;
+        choose_pivot();
+        sweep<kLds>(b0, 0, ns, sh.mge, sh.mle);
+        uint64_t mg[1], ml[1];
+        mg[0] = (uint32_t)lane < ns ? sh.mge[lane] : 0ull;
+        ml[0] = (uint32_t)lane < ns ? sh.mle[lane] : 0ull;
+        const uint32_t cg = (uint32_t)__popcll(mg[0]), cl = (uint32_t)__popcll(ml[0]);
+        const uint32_t gi = wave_incl_scan(cg), li = wave_incl_scan(cl);
+        const uint32_t lt = lane_read(li, 63);
+        const uint32_t gpre = gi - cg, lsuf = lt - (li - cl);
+        // ---- crossing
+        const uint64_t hit = __ballot((uint32_t)lane < ns && gpre < lsuf && gpre + cg >= lsuf - cl);
+        const int sc = __builtin_ctzll(hit);
+        const uint64_t a = lane_read_u64(mg[0], sc), bb = lane_read_u64(ml[0], sc);
+        const uint32_t gcar = lane_read(gpre, sc), lcar = lane_read(lsuf, sc);
+        uint32_t lo = 1, hi = 64;
+        while (lo < hi) {
+            const uint32_t m = (lo + hi) / 2;
+            const uint64_t lm = low_mask(m);
+            if (gcar + (uint32_t)__popcll(a & lm) >= lcar - (uint32_t)__popcll(bb & lm)) hi = m;
+            else lo = m + 1;
         }
-        put_any(first + hole, value);
-    }
-    template <int P>
-    __device__ __forceinline__ void adjust_heap(uint32_t hole, uint32_t len, El value) {
-        const uint32_t top = hole;
-        uint32_t second = hole;
-        while (len >= 1 && second < (len - 1) / 2) {
-            second = 2 * (second + 1);
-            if (less<P>(get_any(first + second), get_any(first + second - 1))) second--;
-            put_any(first + hole, get_any(first + second));
-            hole = second;
-        }
-        if ((len & 1u) == 0 && second == (len - 2) / 2) {
-            second = 2 * (second + 1);
-            put_any(first + hole, get_any(first + second - 1));
-            hole = second - 1;
-        }
-        push_heap<P>(hole, top, value);
-    }
-    template <int P>
-    __device__ __forceinline__ void heap_select(uint32_t middle, uint32_t len) {
-        if (middle >= 2) {
-            uint32_t parent = (middle - 2) / 2;
-            while (true) {
-                adjust_heap<P>(parent, middle, get_any(first + parent));
-                if (parent == 0) break;
-                parent--;
+        const uint32_t g1 = gcar + (uint32_t)__popcll(a & low_mask(lo - 1));
+        const uint32_t l2 = lcar - (uint32_t)__popcll(bb & low_mask(lo));
+        const uint32_t ks = g1 > l2 ? g1 : l2;
+        // ---- partners (lists in LDS) and L_{Ks+1}, L_{Ks}, R_{Ks}: each lane walks its step's bits
+        uint32_t my_cl = kNone, my_cr = kNone, my_lks = kNone;
+        if ((uint32_t)lane < ns) {
+            const uint32_t sb = b0 + 64 * (uint32_t)lane;
+            uint64_t a = mg[0];
+            uint32_t k = gpre + 1;
+            while (a != 0 && k <= ks + 1) {
+                const uint32_t pos = sb + (uint32_t)__builtin_ctzll(a);
+                a &= a - 1;
+                if (k <= ks) sh.lp[k - 1] = (uint16_t)(pos - b0);
+                if (k == ks + 1) my_cl = pos;
+                if (k == ks) my_lks = pos;
+                ++k;
+            }
+            uint64_t bb = ml[0];
+            k = lsuf - (uint32_t)__popcll(bb) + 1;
+            while (bb != 0 && k <= ks) {
+                const uint32_t hb = 63u - (uint32_t)__builtin_clzll(bb);
+                const uint32_t pos = sb + hb;
+                bb &= ~(1ull << hb);
+                sh.rp[k - 1] = (uint16_t)(pos - b0);
+                if (k == ks) my_cr = pos;
+                ++k;
             }
         }
-        for (uint32_t i = middle; i < len; ++i)
-            if (less<P>(get_any(first + i), get_any(first))) {
-                const El v = get_any(first + i);
-                put_any(first + i, get_any(first));
-                adjust_heap<P>(0, middle, v);
+        const uint32_t cut_l = wave_min_u(my_cl), cut_r = wave_min_u(my_cr), l_ks = wave_min_u(my_lks);
+        const uint32_t cut = cut_l < cut_r ? cut_l : cut_r;
+        const bool right = cut <= nth;
+        const uint32_t nf = right ? cut : first, nl = right ? last : cut;
+        if (cut == nth && !rec) lo_el = (ks > 0 && l_ks == cut - 1) ? elp(cut_r) : elp(cut - 1);
+        // ---- swaps, then the median-of-three swap (lane 0; ch's target test from its step's records)
+        const uint32_t s = (pv.ch - b0) / 64, bit = (pv.ch - b0) % 64;
+        const uint64_t ga = lane_read_u64(mg[0], (int)s), la = lane_read_u64(ml[0], (int)s), below = low_mask(bit);
+        const uint32_t g0 = lane_read(gpre, (int)s), l0 = lane_read(lsuf, (int)s);
+        bool tgt = false;
+        if (!right && ((ga >> bit) & 1ull)) tgt = g0 + (uint32_t)__popcll(ga & below) + 1 <= ks;
+        if (right && ((la >> bit) & 1ull)) tgt = l0 - (uint32_t)__popcll(la & below) <= ks;
+        for (uint32_t k0 = (uint32_t)lane; k0 < ks; k0 += 64 * kBatch) {
+            uint32_t to[kBatch];
+            El ev[kBatch];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                const uint32_t k = k0 + (uint32_t)(64 * b);
+                if (k < ks) {
+                    const uint32_t lq = b0 + sh.lp[k], rq = b0 + sh.rp[k];
+                    to[b] = right ? rq : lq;
+                    ev[b] = elp(right ? lq : rq);
+                }
             }
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b)
+                if (k0 + (uint32_t)(64 * b) < ks) put(to[b], ev[b]);
+        }
+        if (lane == 0) {
+            if (first >= nf && first < nl) put(first, pv.e);
+            if (pv.ch >= nf && pv.ch < nl && !tgt) put(pv.ch, pv.f0);
+        }
+        __builtin_amdgcn_wave_barrier();
+        rec = rec || cut == nth;
+        first = nf;
+        last = nl;
     }
 
     // ---------------------------------------------------------------- std::nth_element(vec, vec + nth)
-    // returns (vec[nth - 1], vec[nth]) of the post-state as values (lo only when nth >= 1), on thread 0
-    template <int P>
+    // (vec[nth - 1], vec[nth]) of the post-state as values (lo only when nth >= 1), on thread 0
     __device__ __forceinline__ void select(double& lo, double& hi) {
         first = 0; last = M; base = 0; where = kSrc; rec = 0;
         depth = M > 1 ? 2 * lg2(M) : 0;
         const uint64_t t0 = clock64();
-        uint32_t nglb = 0, nlds = 0;
-        if (last - first > 3) {
-            --depth;
-            round_any<P, kSrc>();
-        }
-        const uint64_t t1 = clock64();
+        uint64_t t1 = t0;
+        uint32_t nblk = 0, nwave = 0;
         while (last - first > 3) {
             if (depth == 0) {
-                if (tid == 0) {
-                    heap_select<P>(nth + 1 - first, last - first);
-                    const El f0 = get_any(first), n0 = get_any(nth);
-                    put_any(first, n0);
-                    put_any(nth, f0);
-                }
+                if (tid == 0)
+                    heap_select_fn<Src, Id>(HeapView<Src, Id>{src, &sh, gkey, gid, first, base, where, P, med},
+                                            nth + 1 - first, last - first, nth - first);
                 __syncthreads();
                 break;
+            }
+            if (where == kLds && last - (first & ~63u) <= 64u * 64u) {  // the rest by wave 0, no barriers
+                if (wave == 0) {
+                    while (last - first > 3 && depth > 0) {
+                        --depth;
+                        wave_round();
+                        ++nwave;
+                    }
+                    if (lane == 0) {
+                        sh.bc_first = first; sh.bc_last = last; sh.bc_depth = (uint32_t)depth; sh.bc_rec = (uint32_t)rec;
+                        sh.lo_el = lo_el;
+                    }
+                }
+                __syncthreads();
+                first = sh.bc_first; last = sh.bc_last; depth = (int)sh.bc_depth; rec = (int)sh.bc_rec; lo_el = sh.lo_el;
+                __syncthreads();
+                continue;  // depth 0 with > 3 left: the heap select above
             }
             --depth;
             if (where == kGlb && last - (first & ~63u) <= (uint32_t)kCap && M <= (sizeof(Id) == 2 ? 65536u : 0xFFFFFFFFu)) {
@@ -583,30 +774,31 @@ struct RefSel {
                 base = nb;
                 __syncthreads();
             }
-            if (where == kLds) { round_any<P, kLds>(); ++nlds; }
-            else { round_any<P, kGlb>(); ++nglb; }
+            round();
+            ++nblk;
+            if (nblk == 1) t1 = clock64();
         }
         if (tid == 0) {
             sh.stamp[4 * P] = t1 - t0;
             sh.stamp[4 * P + 1] = clock64() - t1;
-            sh.stamp[4 * P + 2] = nglb;
-            sh.stamp[4 * P + 3] = nlds;
+            sh.stamp[4 * P + 2] = nblk;
+            sh.stamp[4 * P + 3] = nwave;
             if (last - first <= 3) {  // std::__insertion_sort of the last <= 3
                 const uint32_t n = last - first;
                 El v[3];
-                for (uint32_t i = 0; i < n; ++i) v[i] = get_any(first + i);
+                for (uint32_t i = 0; i < n; ++i) v[i] = get(first + i);
                 for (uint32_t i = 1; i < n; ++i) {
                     const El x = v[i];
                     uint32_t j = i;
-                    while (j > 0 && less<P>(x, v[j - 1])) { v[j] = v[j - 1]; --j; }
+                    while (j > 0 && less(src, P, med, x, v[j - 1])) { v[j] = v[j - 1]; --j; }
                     v[j] = x;
                 }
                 for (uint32_t i = 0; i < n; ++i) sh.fin[i] = v[i];
-                hi = value<P>(sh.fin[nth - first]);
-                if (nth >= 1) lo = value<P>(rec ? lo_el : sh.fin[nth - 1 - first]);
+                hi = value(src, P, med, sh.fin[nth - first]);
+                if (nth >= 1) lo = value(src, P, med, rec ? lo_el : sh.fin[nth - 1 - first]);
             } else {  // heap select ran
-                hi = value<P>(get_any(nth));
-                if (nth >= 1) lo = value<P>(rec ? lo_el : get_any(nth - 1));
+                hi = value(src, P, med, get(nth));
+                if (nth >= 1) lo = value(src, P, med, rec ? lo_el : get(nth - 1));
             }
         }
     }
@@ -618,15 +810,17 @@ template <typename Id, class Src>
 __device__ __forceinline__ void ref_robust_scale(const Src& src, RefShared<Id>& sh, uint32_t* sel, int64_t sel_stride,
                                                  uint32_t M, uint32_t n, double& med, double& mad) {
     const int tid = (int)threadIdx.x;
-    RefSel<Src, Id> s{src, sh};
-    const int64_t q = sel_stride / 4;  // q >= M entries each: keys, ids, then the big segments' step records
+    __shared__ Src src_sh;
+    if (tid == 0) src_sh = src;
+    __syncthreads();
+    RefSel<Src, Id> s{&src_sh, sh};
+    s.kb = src.kbase();
+    const int64_t q = sel_stride / 4;  // q >= M entries each: keys, ids, step records, partner lists
     s.gkey = sel;
     s.gid = sel + q;
     const int64_t steps = (q + 63) / 64 + 1;
     s.gmge = reinterpret_cast<uint64_t*>(sel + 2 * q);
     s.gmle = s.gmge + steps;
-    s.ggpre = reinterpret_cast<uint32_t*>(s.gmle + steps);
-    s.glsuf = s.ggpre + steps;
     s.glp = sel + 3 * q;
     s.grp = sel + 3 * q + q / 2;
     s.M = M;
@@ -634,18 +828,19 @@ __device__ __forceinline__ void ref_robust_scale(const Src& src, RefShared<Id>& 
     s.tid = tid; s.lane = tid & 63; s.wave = tid >> 6;
     s.med = 0.0;
     const bool even = (M & 1u) == 0 && s.nth >= 1;  // mid == 0 (UB in the reference) reads vec[mid]
-    double lo = 0.0, hi = 0.0;
-    s.template select<0>(lo, hi);
     __shared__ double bc;
-    if (tid == 0) bc = even ? (lo + hi) / 2.0 : hi;
-    __syncthreads();
-    s.med = bc;
-    s.template select<1>(lo, hi);
-    if (tid == 0) {
-        med = bc;
-        mad = even ? (lo + hi) / 2.0 : hi;
+    for (int P = 0; P < 2; ++P) {  // one copy of the selection for both passes
+        s.P = P;
+        double lo = 0.0, hi = 0.0;
+        s.select(lo, hi);
+        if (tid == 0) {
+            const double v = even ? (lo + hi) / 2.0 : hi;
+            if (P == 0) { bc = v; med = v; }
+            else mad = v;
+        }
+        __syncthreads();
+        s.med = bc;
     }
-    __syncthreads();
 }
 
 template <typename Id>
@@ -718,14 +913,19 @@ __global__ void __launch_bounds__(kRT, 1) debug_robust_scale_kernel(const double
     __shared__ RefShared<Id> sh;
     if (threadIdx.x < 32) sh.stamp[threadIdx.x] = 0;
     (void)flags;
+    // the keys K1 would have written (res_key32), into the tail of the scratch
+    const int64_t q = sel_stride / 4;
+    uint32_t* keys = sel + 4 * q;  // (svo_debug_robust_scale allocates 5 q)
+    for (uint32_t p = threadIdx.x; p < M; p += kRT) keys[p] = v[p] >= kDblMax ? kKeyInvisible : res_key32(v[p]);
+    __threadfence_block();
     __syncthreads();
-    ArrSrc src{v};
+    ArrSrc src{v, keys};
     double med = 0.0, mad = 0.0;
     ref_robust_scale<Id>(src, sh, sel, sel_stride, M, n, med, mad);
     if (threadIdx.x == 0) {
         out[0] = med;
         out[1] = mad;
-        for (int i = 0; i < 26; ++i) out[2 + i] = (double)sh.stamp[i];
+        for (int i = 0; i < 30; ++i) out[2 + i] = (double)sh.stamp[i];
     }
 }
 

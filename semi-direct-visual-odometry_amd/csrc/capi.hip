@@ -351,6 +351,8 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
                     prm->median_mode);
     const int half = prm->patch_size / 2, area = (2 * half + 1) * (2 * half + 1);
     if ((int64_t)max_features * area >= (1ll << 31)) return fail(SVO_ERR_ARG, "max_features too large");
+    if (prm->median_mode == SVO_MEDIAN_REFERENCE && (int64_t)max_features * area > 524288)
+        return fail(SVO_ERR_ARG, "median_mode 1 supports up to 524288 residual slots per pair (max_features * patch^2)");
     SVO_HIP(hipSetDevice(c->device));
     svo_align_batch* b = new (std::nothrow) svo_align_batch{};
     if (!b) return fail(SVO_ERR_ARG, "out of host memory");
@@ -626,28 +628,28 @@ int svo_align_batch_traces(svo_align_batch* b, int32_t pair, svo_level_trace* ou
 
 int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, int64_t n_valid, double* med_mad) {
     if (!c || !values || !med_mad) return fail(SVO_ERR_ARG, "null argument");
-    if (n_slots < 1 || n_slots >= (1ll << 30) || n_valid < 1 || n_valid > n_slots)
-        return fail(SVO_ERR_ARG, "need 1 <= n_valid <= n_slots < 2^30 (got %lld, %lld)", (long long)n_valid,
+    if (n_slots < 1 || n_slots > 524288 || n_valid < 1 || n_valid > n_slots)
+        return fail(SVO_ERR_ARG, "need 1 <= n_valid <= n_slots <= 524288 (got %lld, %lld)", (long long)n_valid,
                     (long long)n_slots);
     for (int64_t i = 0; i < n_slots; ++i)
         if (!(values[i] >= -255.0 && values[i] <= 255.0) && values[i] != 1.7976931348623157e308)
             return fail(SVO_ERR_ARG, "value %lld = %g outside [-255, 255] and not DBL_MAX", (long long)i, values[i]);
     SVO_HIP(hipSetDevice(c->device));
     const int64_t q = (n_slots + 63) / 64 * 64;
-    const size_t bytes = (size_t)q * 8 + (size_t)4 * q * 4 + 256;
+    const size_t bytes = (size_t)q * 8 + (size_t)5 * q * 4 + 512;
     void* base = nullptr;
     hipError_t e = ctx_scratch(c, bytes, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_debug_robust_scale: %s", hipGetErrorString(e));
     SVO_HIP(ctx_ring_drain(c));
     double* d_v = static_cast<double*>(base);
     uint32_t* d_sel = reinterpret_cast<uint32_t*>(d_v + q);
-    double* d_out = reinterpret_cast<double*>(d_sel + 4 * q);
+    double* d_out = reinterpret_cast<double*>(d_sel + 5 * q);  // after the K2R scratch and the keys
     SVO_HIP(hipMemcpyAsync(d_v, values, (size_t)n_slots * 8, hipMemcpyHostToDevice, c->stream));
     const char* st = getenv("SVO_DEBUG_STAMPS");  // "2": phase stamps of round 1 only (tools/k2r_probe.py)
     svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, 4 * q, d_out,
                                    st && st[0] == '2' ? 1 : 0, c->stream);
     SVO_HIP(hipGetLastError());
-    SVO_HIP(hipMemcpyAsync(med_mad, d_out, getenv("SVO_DEBUG_STAMPS") ? 224 : 16, hipMemcpyDeviceToHost, c->stream));
+    SVO_HIP(hipMemcpyAsync(med_mad, d_out, getenv("SVO_DEBUG_STAMPS") ? 256 : 16, hipMemcpyDeviceToHost, c->stream));
     SVO_HIP(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }

@@ -387,6 +387,12 @@ void Map::addCandidateToFrame(std::shared_ptr<Frame>& frame) {
         c.matched = true;
         m_cellVisited[cells[j]] = 1;
     }
+    removeMatchedCandidate();  // (:626)
+}
+
+void Map::removeMatchedCandidate() {  // src/map.cpp:629-634
+    m_candidates.erase(std::remove_if(m_candidates.begin(), m_candidates.end(), [](const Candidate& c) { return c.matched; }),
+                       m_candidates.end());
 }
 
 // ------------------------------------------------------------------ trajectory / feature dump

@@ -207,6 +207,7 @@ public:
                       std::vector<std::pair<std::shared_ptr<Frame>, int32_t>>& overlapKeyFrames);
     void addNewCandidate(const std::shared_ptr<Feature>& feature, const std::shared_ptr<Point>& point);
     void addCandidateToFrame(std::shared_ptr<Frame>& frame);
+    void removeMatchedCandidate();  // src/map.cpp:629-634
     uint32_t m_matches = 0, m_trials = 0;
     std::vector<int32_t> m_cellOrders;
     std::vector<uint8_t> m_cellVisited;  // never cleared, as in the reference

@@ -173,6 +173,7 @@ int main(int argc, char** argv) {
             const std::vector<uint8_t> rimg = read_raw(argv[3], (size_t)w * h), kimg = read_raw(argv[4], (size_t)w * h),
                                        cimg = read_raw(argv[5], (size_t)w * h);
             const int reps = argc >= 7 ? std::atoi(argv[6]) : 0;  // > 0: time reprojectMap + addCandidateToFrame
+            const bool twice = argc >= 8 && std::string(argv[7]) == "twice";  // then a second addCandidateToFrame
             Context ctx(0);
             auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, fx, fy, cx, cy});
             double total_ms = 0.0;
@@ -210,6 +211,16 @@ int main(int argc, char** argv) {
                     std::printf("counts %u %u\n", map.m_matches, map.m_trials);
                     for (const auto& ft : cur->m_features)
                         std::printf("px %.17g %.17g\n", ft->m_pixelPosition[0], ft->m_pixelPosition[1]);
+                    if (twice) {  // a second frame (cur moved 5 cm along x): only unmatched candidates remain
+                        std::printf("candidates %zu\n", map.m_candidates.size());
+                        auto cur2 = std::make_shared<Frame>(ctx, cam, cimg.data(), 1, kf);
+                        cur2->m_absPose = poses[2];
+                        cur2->m_absPose[4] += 0.05;
+                        map.addCandidateToFrame(cur2);
+                        std::printf("candidates %zu\n", map.m_candidates.size());
+                        for (const auto& ft : cur2->m_features)
+                            std::printf("px2 %.17g %.17g\n", ft->m_pixelPosition[0], ft->m_pixelPosition[1]);
+                    }
                 }
             }
             if (reps > 0) std::printf("ms %.6f\n", total_ms / reps);

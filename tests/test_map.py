@@ -183,3 +183,43 @@ def test_gpu_cpp_mirror_map(tmp_path):
     expect = np.concatenate([rep[1], cpx[cm]])
     assert lines[0] == f"counts {rep[4]} {rep[5]}"
     np.testing.assert_array_equal(got, expect)
+
+
+@pytest.mark.gpu
+def test_gpu_cpp_mirror_add_candidates_twice(tmp_path):
+    """host/svo.hpp Map::addCandidateToFrame removes its matched candidates (src/map.cpp:626, 629-634): a
+    second call, on a frame 5 cm further along x, aligns only the candidates the first call left, against
+    the sequential oracle (same cells visited, same remaining list, same new features bit for bit)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "semi-direct-visual-odometry_amd", "build", "svo_host_check")
+    mp = synth.make_map_problem()
+    c = mp.camera
+    W, H = c["width"], c["height"]
+    ncells = math.ceil(W / mp.cell_size) * math.ceil(H / mp.cell_size)
+    order = np.random.default_rng(5).permutation(ncells).astype(np.int32)
+    paths = synth.write_map_problem(mp, str(tmp_path), order)
+    out = subprocess.run([exe, "map", *paths, "0", "twice"], capture_output=True, text=True, timeout=60, check=True)
+    lines = out.stdout.splitlines()
+    grad = {k: O.unpack_levels(O.build_pyramid(img, 1)[1], W, H, 1)[0]
+            for k, img in (("ref", mp.ref_img), ("kf", mp.kf_img), ("cur", mp.cur_img))}
+    ptype, psucc = mp.point_type.copy(), mp.point_succ.copy()
+    plast = np.full(len(mp.point_pos), np.uint64(2 ** 64 - 1), np.uint64)
+    visited = np.zeros(ncells, np.uint8)
+    O.reproject_map(mp.camera, mp.cell_size, order, mp.cur_pose, 7, grad["cur"], [grad["ref"], grad["kf"]],
+                    np.array([0, mp.n_ref, mp.n_ref + mp.n_kf], np.int32), mp.feat_px, mp.feat_point,
+                    mp.point_pos, ptype, psucc, plast, visited)
+    nc = len(mp.cand_feat)
+    cm, _ = O.add_candidates(mp.camera, mp.cell_size, visited, mp.cur_pose, grad["cur"], [grad["kf"]] * nc,
+                             mp.feat_px[mp.cand_feat], mp.cand_pos)
+    keep = ~cm
+    assert cm.any() and keep.any()
+    pose2 = np.array(mp.cur_pose, np.float64).copy()
+    pose2[4] += 0.05
+    cm2, cpx2 = O.add_candidates(mp.camera, mp.cell_size, visited, pose2, grad["cur"], [grad["kf"]] * int(keep.sum()),
+                                 mp.feat_px[mp.cand_feat][keep], mp.cand_pos[keep])
+    counts = [ln for ln in lines if ln.startswith("candidates ")]
+    assert counts == [f"candidates {int(keep.sum())}", f"candidates {int(keep.sum() - cm2.sum())}"], counts
+    got2 = np.array([[float(v) for v in ln.split()[1:]] for ln in lines if ln.startswith("px2 ")]).reshape(-1, 2)
+    np.testing.assert_array_equal(got2, cpx2[cm2])

@@ -17,7 +17,7 @@ v = rng.normal(0, 8, 50000)
 v[np.repeat(rng.random(2000) < 0.2, 25)] = np.finfo(np.float64).max
 n = int((v < 1e300).sum())
 ctx = svo_amd.default_context()
-out = np.zeros(28)
+out = np.zeros(32)
 for _ in range(3):
     _capi.check(_capi.lib().svo_debug_robust_scale(ctx.handle, _capi.ptr(v), len(v), n, _capi.ptr(out)))
 t0 = time.perf_counter()
@@ -26,9 +26,10 @@ for _ in range(20):
 dt = (time.perf_counter() - t0) / 20
 print(f"med {out[0]!r} mad {out[1]!r}  call {dt * 1e6:.1f} us")
 for p in range(2):
-    r1, rest, ng, nl = out[2 + 4 * p: 6 + 4 * p]
-    print(f"pass {p}: round1 {r1:.0f} cycles, rest {rest:.0f} cycles, global rounds {ng:.0f}, lds rounds {nl:.0f}")
-names = ("pivot", "sweep", "scan", "crossing", "partners", "swaps/copy")
+    r1, rest, nb, nw = out[2 + 4 * p: 6 + 4 * p]
+    print(f"pass {p}: round1 {r1:.0f} cycles, rest {rest:.0f} cycles, block rounds {nb:.0f}, wave rounds {nw:.0f}")
+names = ("pivot", "sweep", "crossing", "partners", "swaps/copy")
 for w, kind in enumerate(("round 1", "global rounds", "lds rounds")):
-    ph = out[10 + 6 * w: 16 + 6 * w]
+    ph = out[10 + 5 * w: 15 + 5 * w]
     print(f"{kind:14s} cycles per phase (both passes): " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, ph)))
+print(f"exact classifications: pass 0 {out[30]:.0f}, pass 1 {out[31]:.0f}")
