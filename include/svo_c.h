@@ -136,12 +136,28 @@ int svo_align_batch_destroy(svo_align_batch* batch);
  *   bearing  (n_ref+n_kf) x 3   Feature::m_bearingVec (include/feature.hpp:33-34)
  *   point    (n_ref+n_kf) x 3   Point::m_position in world coordinates (include/point.hpp:28)
  *   has_point(n_ref+n_kf)       Feature::m_point != nullptr
- * Copies the host arrays to device memory (synchronous). */
+ * The host arrays are consumed on return (copied into the context's pinned staging ring, or read
+ * directly for pairs too large for it); the device copies are stream-ordered before any later work on
+ * the context stream and are not waited for.  A copy that fails after this call returned is reported
+ * by a later call on the context (the next run, results or pinned-memory user). */
 int svo_align_batch_set_pair(svo_align_batch* batch, int32_t pair, const svo_pyramid_set* ref_set, int32_t ref_frame,
                              const svo_pyramid_set* kf_set, int32_t kf_frame, const svo_pyramid_set* cur_set,
                              int32_t cur_frame, const double* ref_pose, const double* kf_pose,
                              const double* cur_pose, int32_t n_ref, int32_t n_kf, const double* px,
                              const double* bearing, const double* point, const uint8_t* has_point);
+/* Describe pairs [first, first + count) in one call (the bulk form of svo_align_batch_set_pair): one copy
+ * per array for all of them, then a device scatter into the pairs' feature slots.
+ *   frames   count x 3   frame indices (ref, kf, cur) in ref_set / kf_set / cur_set
+ *   poses    count x 21  ref, kf, cur poses (7 each, as set_pair)
+ *   n_feat   count x 2   n_ref, n_kf
+ *   px, bearing, point, has_point: the pairs' feature rows packed pair after pair (pair i's rows start at
+ *   the sum of the earlier pairs' n_ref + n_kf), layouts as set_pair.  With features_on_device != 0 they
+ *   are device pointers on the context's device (e.g. FeatureSelection output), else host memory.
+ * Synchronous: every host array is consumed and the copies are complete on return. */
+int svo_align_batch_set_pairs(svo_align_batch* batch, int32_t first, int32_t count, const svo_pyramid_set* ref_set,
+                              const svo_pyramid_set* kf_set, const svo_pyramid_set* cur_set, const int32_t* frames,
+                              const double* poses, const int32_t* n_feat, const double* px, const double* bearing,
+                              const double* point, const uint8_t* has_point, int32_t features_on_device);
 /* Replace the initial cur poses of all pairs (n_pairs x 7).  Synchronous H2D. */
 int svo_align_batch_set_initial_poses(svo_align_batch* batch, const double* poses);
 /* Run every pair.  Asynchronous on the context stream; inputs stay untouched, so repeated runs are

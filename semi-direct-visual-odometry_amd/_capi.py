@@ -69,6 +69,8 @@ _SIGNATURES = [
     ("svo_align_batch_set_pair", c_int32, [c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int32, c_void_p, c_int32,
                                            c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
                                            c_void_p, c_void_p]),
+    ("svo_align_batch_set_pairs", c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32]),
     ("svo_align_batch_set_initial_poses", c_int32, [c_void_p, c_void_p]),
     ("svo_align_batch_run", c_int32, [c_void_p]),
     ("svo_align_batch_profile", c_int32, [c_void_p, ctypes.POINTER(ctypes.c_float)]),

@@ -298,11 +298,12 @@ MEDIAN_EXACT, MEDIAN_REFERENCE = 0, 1  # include/svo_c.h SVO_MEDIAN_*
 class AlignBatch:
     """n_pairs independent ImageAlignment::align problems on one GPU (svo_align_batch).
 
-    median_mode: MEDIAN_REFERENCE reproduces the reference's robust scale bit for bit (libstdc++
-    nth_element post-state, src/algorithm.cpp:834-853); MEDIAN_EXACT uses true order statistics."""
+    median_mode: MEDIAN_REFERENCE (default) reproduces the reference's robust scale bit for bit (libstdc++
+    nth_element post-state, src/algorithm.cpp:834-853); MEDIAN_EXACT uses true order statistics (faster,
+    not the reference's numbers: DESIGN.md)."""
 
     def __init__(self, camera, patch_size, min_level, max_level, n_pairs, max_features, ctx=None,
-                 median_mode=MEDIAN_EXACT):
+                 median_mode=MEDIAN_REFERENCE):
         self.ctx = ctx or default_context()
         self.camera = camera
         self.n_pairs = int(n_pairs)
@@ -326,6 +327,29 @@ class AlignBatch:
                                              int(kf[1]), cur[0].handle, int(cur[1]), *[ptr(p) for p in poses],
                                              int(n_ref), int(n_kf), ptr(px), ptr(bearing), ptr(point), ptr(has_point)))
         self._keep[pair] = (ref[0], kf[0], cur[0])
+
+    def set_pairs(self, first, ref_set, kf_set, cur_set, frames, poses, n_feat, px, bearing, point, has_point):
+        """Bulk set_pair (svo_align_batch_set_pairs) for pairs [first, first + len(frames)): frames (count, 3)
+        (ref, kf, cur) indices into the three PyramidSets, poses (count, 3, 7), n_feat (count, 2) = (n_ref,
+        n_kf), feature rows packed pair after pair.  Feature arrays may be numpy (host) or CUDA tensors
+        (device pointers, copied on the device)."""
+        frames = np.ascontiguousarray(frames, dtype=np.int32).reshape(-1, 3)
+        count = frames.shape[0]
+        poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(count, 21)
+        n_feat = np.ascontiguousarray(n_feat, dtype=np.int32).reshape(count, 2)
+        on_dev = all(hasattr(a, "data_ptr") and getattr(a, "is_cuda", False) for a in (px, bearing, point, has_point))
+        if on_dev:
+            ptrs = [ctypes.c_void_p(a.data_ptr()) for a in (px, bearing, point, has_point)]
+            keep = (px, bearing, point, has_point)
+        else:
+            keep = (np.ascontiguousarray(px, dtype=np.float64), np.ascontiguousarray(bearing, dtype=np.float64),
+                    np.ascontiguousarray(point, dtype=np.float64), np.ascontiguousarray(has_point, dtype=np.uint8))
+            ptrs = [ptr(a) for a in keep]
+        check(lib().svo_align_batch_set_pairs(self.handle, int(first), int(count), ref_set.handle, kf_set.handle,
+                                              cur_set.handle, ptr(frames), ptr(poses), ptr(n_feat), *ptrs, int(on_dev)))
+        for i in range(count):
+            self._keep[int(first) + i] = (ref_set, kf_set, cur_set)
+        del keep
 
     def set_initial_poses(self, poses):
         poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(self.n_pairs, 7)
@@ -369,13 +393,16 @@ class AlignBatch:
 class ImageAlignment:
     """ImageAlignment(patchSize, minLevel, maxLevel, numParameters) (src/image_alignment.cpp:15-67)."""
 
-    def __init__(self, patch_size, min_level, max_level, num_parameters=6, ctx=None):
+    def __init__(self, patch_size, min_level, max_level, num_parameters=6, ctx=None, median_mode=MEDIAN_REFERENCE):
         if num_parameters != 6:
             raise ValueError("ImageAlignment estimates SE(3): numParameters must be 6")
         self.patch_size, self.min_level, self.max_level = int(patch_size), int(min_level), int(max_level)
         self.ctx = ctx or default_context()
+        self.median_mode = int(median_mode)
         self.last_status = None
         self.last_traces = None
+        self._batch = None  # grow-only single-pair batch, reused across align() calls
+        self._batch_key = None
 
     def align(self, ref_frame, cur_frame):
         """Aligns cur_frame.abs_pose in place; returns the finest level's RMSE (0 if ref has no features)."""
@@ -386,16 +413,22 @@ class ImageAlignment:
             raise ValueError("ref_frame.last_keyframe is required (src/image_alignment.cpp:30-31)")
         px, br, pt, hp = _feature_arrays([ref_frame, kf])
         nf = ref_frame.number_observation() + kf.number_observation()
-        b = AlignBatch(ref_frame.camera, self.patch_size, self.min_level, self.max_level, 1, max(nf, 1), self.ctx)
-        try:
-            s = lambda fr: (fr.image_pyramid.set, 0)
-            b.set_pair(0, s(ref_frame), s(kf), s(cur_frame), ref_frame.abs_pose, kf.abs_pose, cur_frame.abs_pose,
-                       ref_frame.number_observation(), kf.number_observation(), px, br, pt, hp)
-            b.run()
-            poses, err, st = b.results()
-            self.last_traces = b.traces(0)
-        finally:
-            b.close()
+        cam = ref_frame.camera
+        key = (cam.width, cam.height, cam.fx, cam.fy, cam.cx, cam.cy)
+        if self._batch is None or self._batch_key != key or self._batch_cap < nf:
+            if self._batch is not None:
+                self._batch.close()
+            cap = max(nf, 1) if self._batch is None else max(nf, 2 * self._batch_cap)
+            self._batch = AlignBatch(cam, self.patch_size, self.min_level, self.max_level, 1, cap, self.ctx,
+                                     median_mode=self.median_mode)
+            self._batch_key, self._batch_cap = key, cap
+        b = self._batch
+        s = lambda fr: (fr.image_pyramid.set, 0)
+        b.set_pair(0, s(ref_frame), s(kf), s(cur_frame), ref_frame.abs_pose, kf.abs_pose, cur_frame.abs_pose,
+                   ref_frame.number_observation(), kf.number_observation(), px, br, pt, hp)
+        b.run()
+        poses, err, st = b.results()
+        self.last_traces = b.traces(0)
         cur_frame.abs_pose[:] = poses[0]
         self.last_status = int(st[0])
         return float(err[0])

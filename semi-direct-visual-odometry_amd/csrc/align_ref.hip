@@ -68,10 +68,11 @@ struct Pivot {
 template <typename Id>
 struct RefShared {
     static constexpr int kCap = sizeof(Id) == 2 ? 16384 : 12288;  // LDS segment capacity (elements)
-    alignas(16) uint32_t key[kCap];          // the segment, from position `base`
+    alignas(16) uint32_t key[kCap + 64];     // the segment, from position `base` (+64: whole-step reads)
     Id id[kCap];
     uint16_t lp[kCap / 2], rp[kCap / 2];     // L_k, R_k - b0 for k <= Ks (LDS rounds)
-    uint64_t mge[kMeta], mle[kMeta];         // per 64-position step: GE / LE ballots (for the crossing search)
+    uint64_t mge[kMeta], mle[kMeta];         // per 64-position step: GE / LE ballots
+    uint32_t gpre[kMeta], lsuf[kMeta];       // per step: #GE before it, #LE from its first position on
     uint32_t wsum[kRW][2];
     Pivot piv;
     uint32_t ks, cut_l, cut_r, l_ks;
@@ -254,6 +255,24 @@ __device__ __attribute__((noinline)) void heap_select_fn(HeapView<Src, Id> h, ui
     h.put(nth_rel, f0);
 }
 
+// block-uniform values read from LDS, moved to scalar registers: the compiler cannot prove them uniform,
+// and control flow on a vector value becomes exec-mask code (every loop over steps, every branch on the
+// round's state)
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni(uint64_t v) { return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v); }
+__device__ __forceinline__ int64_t uni(int64_t v) { return (int64_t)uni((uint64_t)v); }
+__device__ __forceinline__ double uni(double v) { return __builtin_bit_cast(double, uni(__builtin_bit_cast(uint64_t, v))); }
+__device__ __forceinline__ El uni(El e) { return El{uni(e.key), uni(e.id)}; }
+__device__ __forceinline__ Pivot uni(const Pivot& p) {
+    Pivot q;
+    q.e = uni(p.e); q.f0 = uni(p.f0); q.ch = uni(p.ch); q.inv = uni(p.inv);
+    q.plo = uni(p.plo); q.phi = uni(p.phi);
+    q.kA = uni(p.kA); q.kB = uni(p.kB); q.kC = uni(p.kC); q.kD = uni(p.kD);
+    q.tA = uni(p.tA); q.tB = uni(p.tB); q.tC = uni(p.tC); q.tD = uni(p.tD); q.inv_c = uni(p.inv_c);
+    return q;
+}
+
 template <class Src, typename Id>
 struct RefSel {
     using Shared = RefShared<Id>;
@@ -268,6 +287,8 @@ struct RefSel {
     uint32_t* grp;
     uint64_t* gmge;   // step records of segments past kMeta steps (R > 1)
     uint64_t* gmle;
+    uint32_t* ggpre;  // their per-step prefix counts
+    uint32_t* glsuf;
     uint32_t M, nth;
     int tid, lane, wave;
     int P;            // the pass: 0 median, 1 MAD
@@ -352,61 +373,166 @@ struct RefSel {
             if (d0 <= (int64_t)kKeyInvisible - 1) pv.tD = (uint32_t)(d0 < 0 ? 0 : d0);
         }
     }
-    // the class of key k without branches: slow = the keys cannot decide (same cell as the pivot's)
-    template <int PP>
-    __device__ __forceinline__ uint32_t fast_cls(uint32_t k, bool& slow) const {
-        if (PP == 0) {
-            const bool lt = k < pv.e.key, gt = k > pv.e.key;
-            slow = !lt && !gt && k != kKeyInvisible && (k & 1u);
-            return lt ? 2u : (gt ? 1u : 3u);
-        } else {
-            const bool inv = k == kKeyInvisible;
-            const bool ls = k >= pv.tA && k <= pv.tB, gr = k <= pv.tC || k >= pv.tD;
-            slow = !inv && !ls && !gr;
-            return inv ? pv.inv_c : (ls ? 2u : (gr ? 1u : 0u));
-        }
-    }
-    // sweep of steps [s0, s0 + n): step s's GE / LE ballots to mge[s] / mle[s] (lane 0 stores).  The loads
-    // of 8 steps are issued before any is used; the classification is branch-free, the rare key-cell ties
-    // go to classify_slow under one wave-uniform test.
-    template <int W, int PP>
-    __device__ __forceinline__ void sweep_p(uint32_t b0, uint32_t s0, uint32_t n, uint64_t* mge, uint64_t* mle) {
-        for (uint32_t j0 = 0; j0 < n; j0 += 8) {
-            uint32_t kv[8];
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const uint32_t p = b0 + 64 * (s0 + j0 + (uint32_t)b) + (uint32_t)lane;
-                uint32_t k = 0;
-                if (j0 + (uint32_t)b < n && p < last) {
-                    if (W == kLds) k = sh.key[p - base];
-                    else if (W == kGlb) k = gkey[p];
-                    else k = Src::key_at(kb, p);
-                }
-                kv[b] = k;
-            }
-#pragma unroll
-            for (int b = 0; b < 8; ++b) {
-                const uint32_t j = j0 + (uint32_t)b;
-                if (j >= n) break;  // wave-uniform
-                const uint32_t q = b0 + 64 * (s0 + j) + (uint32_t)lane;
-                const uint32_t k = q == pv.ch ? pv.f0.key : kv[b];
-                bool slow;
-                uint32_t c = fast_cls<PP>(k, slow);
-                const bool in = q > first && q < last;  // position first holds the pivot: LE only
-                c = in ? c : (q == first ? 2u : 0u);
-                slow = slow && in;
-                if (__ballot(slow)) {
-                    if (slow) c = classify_slow(src, P, med, k, elp(q).id, pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
-                }
-                const uint64_t bg = __ballot(c & 1u), bl = __ballot(c & 2u);
-                if (lane == 0) { mge[s0 + j] = bg; mle[s0 + j] = bl; }
-            }
-        }
+    // ---------------------------------------------------------------- classification sweep
+    // A step is 64 positions, lane = position.  Its GE / LE masks come straight out of vector compares
+    // (the compare's lane mask IS the ballot): pass 0 ge = (k >= pk), le = (k <= pk); pass 1 from the key
+    // ranges of choose_pivot (lt = [tA, tB], gt = <= tC or >= tD; ge = ~lt, le = ~gt).  Only keys the
+    // compares cannot settle (same inexact cell as the pivot, pass-1 boundary cells) take classify_slow
+    // under one wave-uniform test.  The masks go to the lane that owns the step (writelane), so a wave
+    // holds the records of up to 64 RR steps in registers: lane j of row r = step s0 + 64 r + j.
+    // Positions outside (first, last), `first` itself (the pivot: LE only) and ch (holding f0 after the
+    // median-of-three swap) are fixed afterwards, per record (fix_rows).
+    template <int W>
+    __device__ __forceinline__ uint32_t load_key(uint32_t p) const {
+        if (W == kLds) return sh.key[p - base];
+        if (W == kGlb) return gkey[p];
+        return Src::key_at(kb, p);
     }
     template <int W>
-    __device__ __forceinline__ void sweep(uint32_t b0, uint32_t s0, uint32_t n, uint64_t* mge, uint64_t* mle) {
-        if (P == 0) sweep_p<W, 0>(b0, s0, n, mge, mle);
-        else sweep_p<W, 1>(b0, s0, n, mge, mle);
+    __device__ __forceinline__ uint32_t load_id(uint32_t p) const {
+        if (W == kLds) return (uint32_t)sh.id[p - base];
+        if (W == kGlb) return gid[p];
+        return p;
+    }
+    // bits i with a <= sp + i < b
+    static __device__ __forceinline__ uint64_t range_mask(uint32_t sp, uint32_t a, uint32_t b) {
+        const uint32_t lo = a > sp ? (a - sp < 64u ? a - sp : 64u) : 0u;
+        const uint32_t hi = b > sp ? (b - sp < 64u ? b - sp : 64u) : 0u;
+        return low_mask(hi) & ~low_mask(lo);
+    }
+    template <int W>
+    __device__ __forceinline__ void slow_fix(uint32_t sp, uint32_t k, uint64_t sl, uint64_t& ge, uint64_t& le) const {
+        sl &= range_mask(sp, first + 1, last);
+        const bool me = (sl >> lane) & 1ull;
+        uint32_t c = 0;
+        if (me) c = classify_slow(src, P, med, k, load_id<W>(sp + (uint32_t)lane), pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
+        ge = (ge & ~sl) | __ballot(me && (c & 1u));
+        le = (le & ~sl) | __ballot(me && (c & 2u));
+    }
+    template <int RR, int W, int PP>
+    __device__ __forceinline__ void sweep_rows(uint32_t b0, uint32_t s0, uint32_t n, uint64_t (&mg)[RR], uint64_t (&ml)[RR]) const {
+        const uint32_t pk = __builtin_amdgcn_readfirstlane(pv.e.key);
+        const uint32_t tA = __builtin_amdgcn_readfirstlane(pv.tA), tB = __builtin_amdgcn_readfirstlane(pv.tB);
+        const uint32_t tC = __builtin_amdgcn_readfirstlane(pv.tC), tD = __builtin_amdgcn_readfirstlane(pv.tD);
+        const bool pslow = (pk & 1u) && pk != kKeyInvisible;  // pass 0: equal keys need the exact values
+        const bool pinv = __builtin_amdgcn_readfirstlane(pv.inv) != 0;
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            uint32_t g0 = 0, g1 = 0, l0 = 0, l1 = 0;
+            const uint32_t nr = n > 64u * r ? (n - 64u * r < 64u ? n - 64u * r : 64u) : 0u;
+            const uint32_t sr = s0 + 64u * r;
+            for (uint32_t j0 = 0; j0 < nr; j0 += 8) {
+                uint32_t kv[8];
+#pragma unroll
+                for (int b = 0; b < 8; ++b) kv[b] = load_key<W>(b0 + 64u * (sr + j0 + (uint32_t)b) + (uint32_t)lane);
+#pragma unroll
+                for (int b = 0; b < 8; ++b) {
+                    const uint32_t j = j0 + (uint32_t)b;
+                    if (j >= nr) break;  // wave-uniform
+                    const uint32_t k = kv[b];
+                    uint64_t ge, le, sl;
+                    if (PP == 0) {
+                        ge = __ballot(k >= pk);
+                        le = __ballot(k <= pk);
+                        sl = pslow ? __ballot(k == pk) : 0ull;
+                    } else if (pinv) {  // pivot DBL_MAX: every visible slot is less, DBL_MAX equal
+                        ge = __ballot(k == kKeyInvisible);
+                        le = ~0ull;
+                        sl = 0ull;
+                    } else {
+                        const uint64_t lt = __ballot(k >= tA) & __ballot(k <= tB);
+                        const uint64_t gt = __ballot(k <= tC) | __ballot(k >= tD);
+                        ge = ~lt;
+                        le = ~gt;
+                        sl = ~(lt | gt);
+                    }
+                    if (sl) slow_fix<W>(b0 + 64u * (sr + j), k, sl, ge, le);
+                    g0 = lane_write(g0, (uint32_t)ge, j);
+                    g1 = lane_write(g1, (uint32_t)(ge >> 32), j);
+                    l0 = lane_write(l0, (uint32_t)le, j);
+                    l1 = lane_write(l1, (uint32_t)(le >> 32), j);
+                }
+            }
+            mg[r] = ((uint64_t)g1 << 32) | g0;
+            ml[r] = ((uint64_t)l1 << 32) | l0;
+        }
+    }
+    template <int RR>
+    __device__ __forceinline__ void sweep_rows(uint32_t b0, uint32_t s0, uint32_t n, uint64_t (&mg)[RR], uint64_t (&ml)[RR]) const {
+        if (P == 0) {
+            if (where == kLds) sweep_rows<RR, kLds, 0>(b0, s0, n, mg, ml);
+            else if (where == kGlb) sweep_rows<RR, kGlb, 0>(b0, s0, n, mg, ml);
+            else sweep_rows<RR, kSrc, 0>(b0, s0, n, mg, ml);
+        } else {
+            if (where == kLds) sweep_rows<RR, kLds, 1>(b0, s0, n, mg, ml);
+            else if (where == kGlb) sweep_rows<RR, kGlb, 1>(b0, s0, n, mg, ml);
+            else sweep_rows<RR, kSrc, 1>(b0, s0, n, mg, ml);
+        }
+    }
+    // the records' edge fixes (lanes holding a step of this wave only): GE in (first, last), LE in
+    // [first, last) with `first` LE, ch classified as f0 (f0c)
+    template <int RR>
+    __device__ __forceinline__ void fix_rows(uint32_t b0, uint32_t s0, uint32_t n, uint32_t f0c, uint64_t (&mg)[RR], uint64_t (&ml)[RR]) const {
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const uint32_t j = 64u * r + (uint32_t)lane;
+            const uint32_t sp = b0 + 64u * (s0 + j);
+            if (j < n) {
+                mg[r] &= range_mask(sp, first + 1, last);
+                ml[r] &= range_mask(sp, first, last);
+                if (first >= sp && first < sp + 64u) ml[r] |= 1ull << (first - sp);
+                if (pv.ch >= sp && pv.ch < sp + 64u) {
+                    const uint64_t bit = 1ull << (pv.ch - sp);
+                    mg[r] = (mg[r] & ~bit) | ((f0c & 1u) ? bit : 0ull);
+                    ml[r] = (ml[r] & ~bit) | ((f0c & 2u) ? bit : 0ull);
+                }
+            } else {
+                mg[r] = 0ull;
+                ml[r] = 0ull;
+            }
+        }
+    }
+    // ---------------------------------------------------------------- swap partners, lane = position
+    // Over the steps a wave holds in registers (lane j of row r = step s0 + 64 r + j: records mg / ml and
+    // the prefix counts gp = #GE before the step, ls = #LE from its start on), read per step with readlane:
+    // the GE of rank k = gp + (GE bits below) + 1 is L_k, the LE of right-rank k = ls - (LE bits below) is
+    // R_k; k <= Ks go to the lists, L_{Ks+1} / L_{Ks} / R_{Ks} to the shared scalars (one position holds
+    // each rank, so one lane writes each).  A step whose ranks all exceed Ks + 1 is skipped (uniform test):
+    // left of the crossing only the GE part runs, right of it only the LE part.
+    template <int RR>
+    __device__ __forceinline__ void partners(uint32_t b0, uint32_t s0, uint32_t n, uint32_t ks, const uint64_t (&mg)[RR],
+                                             const uint64_t (&ml)[RR], const uint32_t (&gp)[RR], const uint32_t (&ls)[RR],
+                                             bool lds_lists) {
+        const uint64_t mybit = 1ull << lane;
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const uint32_t nr = n > 64u * r ? (n - 64u * r < 64u ? n - 64u * r : 64u) : 0u;
+            for (uint32_t j = 0; j < nr; ++j) {
+                const uint32_t g = lane_read(gp[r], (int)j), l = lane_read(ls[r], (int)j);
+                const uint32_t pos = b0 + 64u * (s0 + 64u * r + j) + (uint32_t)lane;
+                if (g <= ks) {
+                    const uint64_t a = lane_read_u64(mg[r], (int)j);
+                    if (a & mybit) {
+                        const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(a >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a, g + 1u));
+                        if (k <= ks) {
+                            if (lds_lists) sh.lp[k - 1] = (uint16_t)(pos - b0);
+                            else glp[k - 1] = pos;
+                        }
+                        if (k == ks + 1u) sh.cut_l = pos;
+                        if (k == ks) sh.l_ks = pos;
+                    }
+                }
+                const uint64_t bb = lane_read_u64(ml[r], (int)j);
+                if (l - (uint32_t)__popcll(bb) < ks && (bb & mybit)) {
+                    const uint32_t k = l - lanes_below(bb);
+                    if (k <= ks) {
+                        if (lds_lists) sh.rp[k - 1] = (uint16_t)(pos - b0);
+                        else grp[k - 1] = pos;
+                        if (k == ks) sh.cut_r = pos;
+                    }
+                }
+            }
+        }
     }
 
     // ---------------------------------------------------------------- one block round (large segments)
@@ -420,6 +546,8 @@ struct RefSel {
         const uint32_t spw = (ns + kRW - 1) / kRW;
         uint64_t* const mge = R <= 2 ? sh.mge : gmge;
         uint64_t* const mle = R <= 2 ? sh.mle : gmle;
+        uint32_t* const mgp = R <= 2 ? sh.gpre : ggpre;
+        uint32_t* const mls = R <= 2 ? sh.lsuf : glsuf;
         uint64_t tp = clock64();
         auto phase = [&](int i) {
             if (tid == 0) { const uint64_t t = clock64(); sh.stamp[8 + 5 * where + i] += t - tp; tp = t; }
@@ -432,22 +560,20 @@ struct RefSel {
             }
         }
         __syncthreads();
-        pv = sh.piv;
+        pv = uni(sh.piv);
         phase(0);
-        // ---- classification sweep of the wave's steps
+        // ---- classification sweep of the wave's steps, records in registers, then to the step arrays
         const uint32_t ws0 = (uint32_t)wave * spw;
         const uint32_t wsn = ws0 >= ns ? 0u : (ns - ws0 < spw ? ns - ws0 : spw);
-        if (where == kLds) sweep<kLds>(b0, ws0, wsn, mge, mle);
-        else if (where == kGlb) sweep<kGlb>(b0, ws0, wsn, mge, mle);
-        else sweep<kSrc>(b0, ws0, wsn, mge, mle);
-        if (R > 2) __threadfence_block();  // global step records: lane 0's stores before the lanes' loads
+        const uint32_t f0c = classify(pv.f0.key, pv.ch);
         uint64_t mg[R], ml[R];
+        sweep_rows<R>(b0, ws0, wsn, mg, ml);
+        fix_rows<R>(b0, ws0, wsn, f0c, mg, ml);
         uint32_t gex[R], lex[R], gw = 0, lw = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t j = 64 * (uint32_t)r + (uint32_t)lane;
-            mg[r] = j < wsn ? mge[ws0 + j] : 0ull;
-            ml[r] = j < wsn ? mle[ws0 + j] : 0ull;
+            if (j < wsn) { mge[ws0 + j] = mg[r]; mle[ws0 + j] = ml[r]; }
             const uint32_t cg = (uint32_t)__popcll(mg[r]), cl = (uint32_t)__popcll(ml[r]);
             const uint32_t gi = wave_incl_scan(cg), li = wave_incl_scan(cl);
             gex[r] = gw + gi - cg;
@@ -456,14 +582,20 @@ struct RefSel {
             lw += lane_read(li, 63);
         }
         if (lane == 0) { sh.wsum[wave][0] = gw; sh.wsum[wave][1] = lw; }
+        if (R > 2) __threadfence_block();  // global step records before the barrier
         __syncthreads();
         phase(1);
-        // ---- wave prefixes (lane i < 16 holds wave i's totals); the crossing t* (first split with G >= Lc):
-        // its wave, its step, its bit, Ks = max(G(t*-1), Lc(t*)), found by wave 0
+        // ---- wave prefixes (lane i < kRW holds wave i's totals), the per-step prefix arrays; the crossing t*
+        // (first split with G >= Lc): its wave, its step, its bit, Ks = max(G(t*-1), Lc(t*)), found by wave 0
         const uint32_t wg = lane < kRW ? sh.wsum[lane][0] : 0u, wl = lane < kRW ? sh.wsum[lane][1] : 0u;
         const uint32_t wgi = wave_incl_scan(wg), wli = wave_incl_scan(wl);
         const uint32_t lt = lane_read(wli, 63);
         const uint32_t gb = lane_read(wgi - wg, wave), lb = lane_read(wli - wl, wave);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t j = 64 * (uint32_t)r + (uint32_t)lane;
+            if (j < wsn) { mgp[ws0 + j] = gb + gex[r]; mls[ws0 + j] = lt - lb - lex[r]; }
+        }
         if (wave == 0) {
             const uint32_t g_start = wgi - wg, l_start = lt - (wli - wl);
             const uint32_t wc = (uint32_t)__builtin_ctzll(__ballot(lane < kRW && g_start < l_start && g_start + wg >= l_start - wl));
@@ -498,48 +630,19 @@ struct RefSel {
             const uint32_t l2 = lcar - (uint32_t)__popcll(bb & low_mask(lo));
             if (lane == 0) sh.ks = g1 > l2 ? g1 : l2;
         }
+        if (R > 2) __threadfence_block();
         __syncthreads();
         phase(2);
-        const uint32_t ks = sh.ks;
-        uint32_t gpre[R], lsuf[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) { gpre[r] = gb + gex[r]; lsuf[r] = lt - lb - lex[r]; }
-        // ---- the swap partners: each lane walks the set bits of its own steps.  L_k (GE rank k <= Ks) and
-        // R_k (LE rank k from the right) to the lists; L_{Ks+1}, L_{Ks}, R_{Ks} to shared scalars
+        const uint32_t ks = uni(sh.ks);
+        // ---- the swap partners of the wave's steps
         const bool lds_lists = where == kLds;
+        uint32_t gpr[R], lsr[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t j = 64 * (uint32_t)r + (uint32_t)lane;
-            if (j >= wsn) continue;
-            const uint32_t sb = b0 + 64 * (ws0 + j);  // the step's first position
-            uint64_t a = mg[r];
-            uint32_t k = gpre[r] + 1;  // GE ranks, ascending with the bit
-            while (a != 0 && k <= ks + 1) {
-                const uint32_t pos = sb + (uint32_t)__builtin_ctzll(a);
-                a &= a - 1;
-                if (k <= ks) {
-                    if (lds_lists) sh.lp[k - 1] = (uint16_t)(pos - b0);
-                    else glp[k - 1] = pos;
-                }
-                if (k == ks + 1) sh.cut_l = pos;
-                if (k == ks) sh.l_ks = pos;
-                ++k;
-            }
-            uint64_t bb = ml[r];
-            k = lsuf[r] - (uint32_t)__popcll(bb) + 1;  // LE right-ranks, ascending downwards from the top bit
-            while (bb != 0 && k <= ks) {
-                const uint32_t hb = 63u - (uint32_t)__builtin_clzll(bb);
-                const uint32_t pos = sb + hb;
-                bb &= ~(1ull << hb);
-                if (lds_lists) sh.rp[k - 1] = (uint16_t)(pos - b0);
-                else grp[k - 1] = pos;
-                if (k == ks) sh.cut_r = pos;
-                ++k;
-            }
-        }
+        for (int r = 0; r < R; ++r) { gpr[r] = gb + gex[r]; lsr[r] = lt - lb - lex[r]; }
+        partners<R>(b0, ws0, wsn, ks, mg, ml, gpr, lsr, lds_lists);
         __syncthreads();
         phase(3);
-        const uint32_t cut_l = sh.cut_l, cut_r = ks > 0 ? sh.cut_r : kNone;
+        const uint32_t cut_l = uni(sh.cut_l), cut_r = ks > 0 ? uni(sh.cut_r) : kNone;
         const uint32_t cut = cut_l < cut_r ? cut_l : cut_r;
         const bool right = cut <= nth;  // the side introselect continues with
         const uint32_t nf = right ? cut : first, nl = right ? last : cut;
@@ -620,9 +723,7 @@ struct RefSel {
                 if (pv.ch >= nf && pv.ch < nl) {  // is ch a swap target? its ranks from the step records
                     const uint32_t s = (pv.ch - b0) / 64, bit = (pv.ch - b0) % 64;
                     const uint64_t below = low_mask(bit), a = mge[s], bb = mle[s];
-                    const uint32_t ow = s / spw;
-                    uint32_t g0 = lane_read(wgi - wg, (int)ow), l0 = lt - lane_read(wli - wl, (int)ow);
-                    for (uint32_t t = ow * spw; t < s; ++t) { g0 += (uint32_t)__popcll(mge[t]); l0 -= (uint32_t)__popcll(mle[t]); }
+                    const uint32_t g0 = mgp[s], l0 = mls[s];
                     bool tgt = false;
                     if (!right && ((a >> bit) & 1ull)) tgt = g0 + (uint32_t)__popcll(a & below) + 1 <= ks;
                     if (right && ((bb >> bit) & 1ull)) tgt = l0 - (uint32_t)__popcll(bb & below) <= ks;
@@ -643,11 +744,20 @@ struct RefSel {
     // earlier instruction.
     __device__ __forceinline__ void wave_round() {
         const uint32_t b0 = first & ~63u, ns = (last - b0 + 63) / 64;
+        uint64_t tp = clock64();
+        auto phase = [&](int i) {  // diagnostics: cycles per phase of the wave rounds
+            if (lane == 0) { const uint64_t t = clock64(); sh.stamp[23 + i] += t - tp; tp = t; }
+        };
         choose_pivot();
-        sweep<kLds>(b0, 0, ns, sh.mge, sh.mle);
+        pv = uni(pv);
+        if (lane == 0) { sh.cut_l = kNone; sh.cut_r = kNone; sh.l_ks = kNone; }
+        const uint32_t f0c = classify(pv.f0.key, pv.ch);
         uint64_t mg[1], ml[1];
-        mg[0] = (uint32_t)lane < ns ? sh.mge[lane] : 0ull;
-        ml[0] = (uint32_t)lane < ns ? sh.mle[lane] : 0ull;
+        phase(0);
+        if (P == 0) sweep_rows<1, kLds, 0>(b0, 0, ns, mg, ml);
+        else sweep_rows<1, kLds, 1>(b0, 0, ns, mg, ml);
+        fix_rows<1>(b0, 0, ns, f0c, mg, ml);
+        phase(1);
         const uint32_t cg = (uint32_t)__popcll(mg[0]), cl = (uint32_t)__popcll(ml[0]);
         const uint32_t gi = wave_incl_scan(cg), li = wave_incl_scan(cl);
         const uint32_t lt = lane_read(li, 63);
@@ -667,32 +777,16 @@ struct RefSel {
         const uint32_t g1 = gcar + (uint32_t)__popcll(a & low_mask(lo - 1));
         const uint32_t l2 = lcar - (uint32_t)__popcll(bb & low_mask(lo));
         const uint32_t ks = g1 > l2 ? g1 : l2;
-        // ---- partners (lists in LDS) and L_{Ks+1}, L_{Ks}, R_{Ks}: each lane walks its step's bits
-        uint32_t my_cl = kNone, my_cr = kNone, my_lks = kNone;
-        if ((uint32_t)lane < ns) {
-            const uint32_t sb = b0 + 64 * (uint32_t)lane;
-            uint64_t a = mg[0];
-            uint32_t k = gpre + 1;
-            while (a != 0 && k <= ks + 1) {
-                const uint32_t pos = sb + (uint32_t)__builtin_ctzll(a);
-                a &= a - 1;
-                if (k <= ks) sh.lp[k - 1] = (uint16_t)(pos - b0);
-                if (k == ks + 1) my_cl = pos;
-                if (k == ks) my_lks = pos;
-                ++k;
-            }
-            uint64_t bb = ml[0];
-            k = lsuf - (uint32_t)__popcll(bb) + 1;
-            while (bb != 0 && k <= ks) {
-                const uint32_t hb = 63u - (uint32_t)__builtin_clzll(bb);
-                const uint32_t pos = sb + hb;
-                bb &= ~(1ull << hb);
-                sh.rp[k - 1] = (uint16_t)(pos - b0);
-                if (k == ks) my_cr = pos;
-                ++k;
-            }
+        // ---- partners (lists in LDS) and L_{Ks+1}, L_{Ks}, R_{Ks}
+        {
+            const uint32_t gpr[1] = {gpre}, lsr[1] = {lsuf};
+            phase(2);
+            partners<1>(b0, 0, ns, ks, mg, ml, gpr, lsr, true);
         }
-        const uint32_t cut_l = wave_min_u(my_cl), cut_r = wave_min_u(my_cr), l_ks = wave_min_u(my_lks);
+        const uint32_t cut_l = __builtin_amdgcn_readfirstlane(sh.cut_l);
+        phase(3);
+        const uint32_t cut_r = __builtin_amdgcn_readfirstlane(sh.cut_r);
+        const uint32_t l_ks = __builtin_amdgcn_readfirstlane(sh.l_ks);
         const uint32_t cut = cut_l < cut_r ? cut_l : cut_r;
         const bool right = cut <= nth;
         const uint32_t nf = right ? cut : first, nl = right ? last : cut;
@@ -725,6 +819,7 @@ struct RefSel {
             if (pv.ch >= nf && pv.ch < nl && !tgt) put(pv.ch, pv.f0);
         }
         __builtin_amdgcn_wave_barrier();
+        phase(4);
         rec = rec || cut == nth;
         first = nf;
         last = nl;
@@ -759,7 +854,8 @@ struct RefSel {
                     }
                 }
                 __syncthreads();
-                first = sh.bc_first; last = sh.bc_last; depth = (int)sh.bc_depth; rec = (int)sh.bc_rec; lo_el = sh.lo_el;
+                first = uni(sh.bc_first); last = uni(sh.bc_last); depth = (int)uni(sh.bc_depth); rec = (int)uni(sh.bc_rec);
+                lo_el = uni(sh.lo_el);
                 __syncthreads();
                 continue;  // depth 0 with > 3 left: the heap select above
             }
@@ -821,11 +917,13 @@ __device__ __forceinline__ void ref_robust_scale(const Src& src, RefShared<Id>& 
     const int64_t steps = (q + 63) / 64 + 1;
     s.gmge = reinterpret_cast<uint64_t*>(sel + 2 * q);
     s.gmle = s.gmge + steps;
+    s.ggpre = reinterpret_cast<uint32_t*>(s.gmle + steps);
+    s.glsuf = s.ggpre + steps;
     s.glp = sel + 3 * q;
     s.grp = sel + 3 * q + q / 2;
     s.M = M;
     s.nth = n / 2;
-    s.tid = tid; s.lane = tid & 63; s.wave = tid >> 6;
+    s.tid = tid; s.lane = tid & 63; s.wave = uni(tid >> 6);
     s.med = 0.0;
     const bool even = (M & 1u) == 0 && s.nth >= 1;  // mid == 0 (UB in the reference) reads vec[mid]
     __shared__ double bc;
@@ -839,7 +937,7 @@ __device__ __forceinline__ void ref_robust_scale(const Src& src, RefShared<Id>& 
             else mad = v;
         }
         __syncthreads();
-        s.med = bc;
+        s.med = uni(bc);
     }
 }
 

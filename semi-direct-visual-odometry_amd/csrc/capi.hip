@@ -162,6 +162,8 @@ struct svo_align_batch {
     int32_t* d_status;
     svo_level_trace* d_traces;
     bool ran;
+    uint8_t* d_stage = nullptr;  // svo_align_batch_set_pairs: packed features + row offsets (grow-only)
+    size_t stage_bytes = 0;
 };
 
 extern "C" {
@@ -332,7 +334,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 static void free_batch(svo_align_batch* b) {
     void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_keys, b->d_keys32, b->d_sel,
                     b->d_state, b->d_partials, b->d_arrive, b->d_fvis, b->d_cproj, b->d_scratch, b->d_pose_out, b->d_err, b->d_status, b->d_traces,
-                    b->d_win};
+                    b->d_win, b->d_stage};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -472,6 +474,10 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
     if (need <= kPinnedCap && ctx_pinned_alloc(c) == hipSuccess) {
         if (c->ring_off + need > kPinnedCap) SVO_HIP(ctx_ring_drain(c));
         char* h = static_cast<char*>(c->pinned) + c->ring_off;
+        // claim the slice before enqueueing: if an enqueue fails part way, copies already queued may still
+        // read it, so the ring stays pending (the next pinned user drains it) and the slice is not reused
+        c->ring_off += need;
+        c->ring_pending = true;
         std::memcpy(h, &d, sizeof(d));
         char* hp = h + r8(sizeof(d));
         if (nf > 0) {
@@ -485,8 +491,6 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
             SVO_HIP(hipMemcpyAsync(b->d_has_point + fo, hp + n * 64, n, hipMemcpyHostToDevice, s));
         }
         SVO_HIP(hipMemcpyAsync(b->d_pairs + pair, h, sizeof(d), hipMemcpyHostToDevice, s));
-        c->ring_off += need;
-        c->ring_pending = true;
     } else {
         (void)hipGetLastError();
         SVO_HIP(ctx_ring_drain(c));
@@ -500,6 +504,103 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
         SVO_HIP(hipStreamSynchronize(s));
     }
     b->pair_set[pair] = 1;
+    return SVO_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// svo_align_batch_set_pairs: pair i's packed rows [off[i], off[i+1]) to its slots from (first + i) * max_f.
+// One workgroup per pair; each array is copied as a flat run of its elements (coalesced both sides).
+__global__ void scatter_features_kernel(const int64_t* __restrict__ off, const double* __restrict__ px,
+                                        const double* __restrict__ bearing, const double* __restrict__ point,
+                                        const uint8_t* __restrict__ has_point, double* __restrict__ dpx,
+                                        double* __restrict__ dbearing, double* __restrict__ dpoint,
+                                        uint8_t* __restrict__ dhas, int32_t first, int32_t max_f) {
+    const int64_t o = off[blockIdx.x], n = off[blockIdx.x + 1] - o;
+    const int64_t d = (int64_t)(first + (int32_t)blockIdx.x) * max_f;
+    for (int64_t e = threadIdx.x; e < 2 * n; e += blockDim.x) dpx[2 * d + e] = px[2 * o + e];
+    for (int64_t e = threadIdx.x; e < 3 * n; e += blockDim.x) dbearing[3 * d + e] = bearing[3 * o + e];
+    for (int64_t e = threadIdx.x; e < 3 * n; e += blockDim.x) dpoint[3 * d + e] = point[3 * o + e];
+    for (int64_t e = threadIdx.x; e < n; e += blockDim.x) dhas[d + e] = has_point[o + e];
+}
+}  // namespace
+
+extern "C" {
+
+int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, const svo_pyramid_set* ref_set,
+                              const svo_pyramid_set* kf_set, const svo_pyramid_set* cur_set, const int32_t* frames,
+                              const double* poses, const int32_t* n_feat, const double* px, const double* bearing,
+                              const double* point, const uint8_t* has_point, int32_t features_on_device) {
+    if (!b || !frames || !poses || !n_feat) return fail(SVO_ERR_ARG, "null argument");
+    if (first < 0 || count < 0 || (int64_t)first + count > b->n_pairs)
+        return fail(SVO_ERR_ARG, "pairs [%d, %d) out of range (n_pairs %d)", first, first + count, b->n_pairs);
+    if (count == 0) return SVO_OK;
+    std::vector<int64_t> off((size_t)count + 1, 0);
+    int rc;
+    for (int32_t i = 0; i < count; ++i) {
+        const int32_t n_ref = n_feat[2 * i], n_kf = n_feat[2 * i + 1];
+        if (n_ref < 0 || n_kf < 0 || n_ref + n_kf > b->max_f)
+            return fail(SVO_ERR_ARG, "pair %d: n_ref+n_kf = %d exceeds max_features %d", first + i, n_ref + n_kf, b->max_f);
+        if ((rc = check_frame(b, ref_set, frames[3 * i])) != SVO_OK) return rc;
+        if ((rc = check_frame(b, kf_set, frames[3 * i + 1])) != SVO_OK) return rc;
+        if ((rc = check_frame(b, cur_set, frames[3 * i + 2])) != SVO_OK) return rc;
+        off[i + 1] = off[i] + n_ref + n_kf;
+    }
+    const int64_t T = off[count];
+    if (T > 0 && (!px || !bearing || !point || !has_point)) return fail(SVO_ERR_ARG, "null feature array");
+    SVO_HIP(hipSetDevice(b->ctx->device));
+    for (int32_t i = 0; i < count; ++i) {
+        svo::PairDesc& d = b->h_pairs[first + i];
+        d.ref_pyr = ref_set->d_base + (size_t)frames[3 * i] * ref_set->stride;
+        d.kf_pyr = kf_set->d_base + (size_t)frames[3 * i + 1] * kf_set->stride;
+        d.cur_pyr = cur_set->d_base + (size_t)frames[3 * i + 2] * cur_set->stride;
+        std::memcpy(d.ref_pose, poses + 21 * i, 7 * sizeof(double));
+        std::memcpy(d.kf_pose, poses + 21 * i + 7, 7 * sizeof(double));
+        std::memcpy(d.cur_pose, poses + 21 * i + 14, 7 * sizeof(double));
+        d.n_ref = n_feat[2 * i];
+        d.n_kf = n_feat[2 * i + 1];
+    }
+    // device staging: the row offsets, then (host features) the packed arrays
+    const size_t off_bytes = ((size_t)(count + 1) * sizeof(int64_t) + 255) / 256 * 256;
+    const size_t host_bytes = features_on_device ? 0 : (size_t)T * 65 + 4 * 256;
+    const size_t need = off_bytes + host_bytes;
+    if (need > b->stage_bytes) {
+        if (b->d_stage) SVO_HIP(hipFree(b->d_stage));
+        b->d_stage = nullptr;
+        b->stage_bytes = 0;
+        SVO_HIP(hipMalloc(&b->d_stage, need + need / 4));
+        b->stage_bytes = need + need / 4;
+    }
+    svo_ctx* c = b->ctx;
+    hipStream_t s = c->stream;
+    SVO_HIP(ctx_ring_drain(c));  // set_pair copies still reading the ring go first (stream order anyway)
+    int64_t* d_off = reinterpret_cast<int64_t*>(b->d_stage);
+    SVO_HIP(hipMemcpyAsync(d_off, off.data(), (size_t)(count + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    SVO_HIP(hipMemcpyAsync(b->d_pairs + first, b->h_pairs.data() + first, sizeof(svo::PairDesc) * count,
+                           hipMemcpyHostToDevice, s));
+    const double *spx = px, *sbr = bearing, *spt = point;
+    const uint8_t* shp = has_point;
+    if (!features_on_device && T > 0) {
+        auto r256 = [](size_t v) { return (v + 255) / 256 * 256; };
+        uint8_t* p = b->d_stage + off_bytes;
+        double* dpx = reinterpret_cast<double*>(p);
+        double* dbr = reinterpret_cast<double*>(p + r256((size_t)T * 16));
+        double* dpt = reinterpret_cast<double*>(p + r256((size_t)T * 16) + r256((size_t)T * 24));
+        uint8_t* dhp = p + r256((size_t)T * 16) + 2 * r256((size_t)T * 24);
+        SVO_HIP(hipMemcpyAsync(dpx, px, (size_t)T * 16, hipMemcpyHostToDevice, s));
+        SVO_HIP(hipMemcpyAsync(dbr, bearing, (size_t)T * 24, hipMemcpyHostToDevice, s));
+        SVO_HIP(hipMemcpyAsync(dpt, point, (size_t)T * 24, hipMemcpyHostToDevice, s));
+        SVO_HIP(hipMemcpyAsync(dhp, has_point, (size_t)T, hipMemcpyHostToDevice, s));
+        spx = dpx; sbr = dbr; spt = dpt; shp = dhp;
+    }
+    if (T > 0)
+        hipLaunchKernelGGL(scatter_features_kernel, dim3(count), dim3(256), 0, s, d_off, spx, sbr, spt, shp, b->d_px,
+                           b->d_bearing, b->d_point, b->d_has_point, first, b->max_f);
+    SVO_HIP(hipGetLastError());
+    // the offsets and descriptors are read from host memory this call owns: wait for them
+    SVO_HIP(hipStreamSynchronize(s));
+    for (int32_t i = 0; i < count; ++i) b->pair_set[first + i] = 1;
     return SVO_OK;
 }
 

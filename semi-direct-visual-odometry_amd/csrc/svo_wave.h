@@ -20,6 +20,11 @@ __device__ __forceinline__ double dpp_mov(double v) {
     return __builtin_bit_cast(double, make_uint2(dpp_mov<kCtrl>(u.x), dpp_mov<kCtrl>(u.y)));
 }
 __device__ __forceinline__ uint32_t lane_read(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+// v_writelane_b32 (no clang builtin on this toolchain: the LLVM intrinsic by name): lane l of `old` := v
+__device__ int svo_writelane_i32(int v, int l, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t lane_write(uint32_t old, uint32_t v, uint32_t l) {
+    return (uint32_t)svo_writelane_i32((int)v, (int)l, (int)old);
+}
 __device__ __forceinline__ double lane_read(double v, int l) {
     const uint2 u = __builtin_bit_cast(uint2, v);
     return __builtin_bit_cast(double, make_uint2(lane_read(u.x, l), lane_read(u.y, l)));

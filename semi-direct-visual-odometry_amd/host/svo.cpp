@@ -1,4 +1,5 @@
 // svo.cpp — implementation of the C++ class-surface mirror (host/svo.hpp) over the C ABI.
+#include <cstring>
 #include "svo.hpp"
 
 #include <algorithm>
@@ -75,41 +76,46 @@ Frame::Frame(Context& ctx, std::shared_ptr<PinholeCamera> camera, const uint8_t*
     m_imagePyramid.createImagePyramid(img, m_camera->width, m_camera->height, maxImagePyramid);
 }
 
-ImageAlignment::ImageAlignment(Context& ctx, uint32_t patchSize, int32_t minLevel, int32_t maxLevel, uint32_t numParameters)
-    : m_ctx(ctx), m_params{(int32_t)patchSize, minLevel, maxLevel, 0} {
+ImageAlignment::ImageAlignment(Context& ctx, uint32_t patchSize, int32_t minLevel, int32_t maxLevel, uint32_t numParameters,
+                               int32_t medianMode)
+    : m_ctx(ctx), m_params{(int32_t)patchSize, minLevel, maxLevel, medianMode} {
     if (numParameters != 6) throw Error(SVO_ERR_ARG, "ImageAlignment: numParameters must be 6");
+}
+
+ImageAlignment::~ImageAlignment() {
+    if (m_batch) svo_align_batch_destroy(m_batch);
 }
 
 double ImageAlignment::align(std::shared_ptr<Frame>& refFrame, std::shared_ptr<Frame>& curFrame) {
     if (refFrame->numberObservation() == 0) return 0;  // src/image_alignment.cpp:27-28
     const auto& kf = refFrame->m_lastKeyframe;
     const int32_t nr = (int32_t)refFrame->numberObservation(), nk = (int32_t)kf->numberObservation();
-    std::vector<double> px, br, pt;
-    std::vector<uint8_t> hp;
+    m_px.clear(); m_br.clear(); m_pt.clear(); m_hp.clear();
     for (const auto* fr : {refFrame.get(), kf.get()})
         for (const auto& f : fr->m_features) {
-            px.insert(px.end(), f->m_pixelPosition.begin(), f->m_pixelPosition.end());
-            br.insert(br.end(), f->m_bearingVec.begin(), f->m_bearingVec.end());
+            m_px.insert(m_px.end(), f->m_pixelPosition.begin(), f->m_pixelPosition.end());
+            m_br.insert(m_br.end(), f->m_bearingVec.begin(), f->m_bearingVec.end());
             const Vec3 p = f->m_point ? f->m_point->m_position : Vec3{0, 0, 0};
-            pt.insert(pt.end(), p.begin(), p.end());
-            hp.push_back(f->m_point ? 1 : 0);
+            m_pt.insert(m_pt.end(), p.begin(), p.end());
+            m_hp.push_back(f->m_point ? 1 : 0);
         }
-    svo_camera cam = refFrame->m_camera->c();
-    svo_align_batch* b = nullptr;
-    check(svo_align_batch_create(m_ctx.get(), &cam, &m_params, 1, nr + nk, &b));
-    double err = 0.0;
-    try {
-        check(svo_align_batch_set_pair(b, 0, refFrame->m_imagePyramid.set(), 0, kf->m_imagePyramid.set(), 0,
-                                       curFrame->m_imagePyramid.set(), 0, refFrame->m_absPose.data(),
-                                       kf->m_absPose.data(), curFrame->m_absPose.data(), nr, nk, px.data(), br.data(),
-                                       pt.data(), hp.data()));
-        check(svo_align_batch_run(b));
-        check(svo_align_batch_results(b, curFrame->m_absPose.data(), &err, &m_status));
-    } catch (...) {
-        svo_align_batch_destroy(b);
-        throw;
+    const svo_camera cam = refFrame->m_camera->c();
+    const bool same_cam = m_batch && std::memcmp(&cam, &m_batchCam, sizeof(cam)) == 0;
+    if (!same_cam || nr + nk > m_batchCap) {  // grow-only: a new batch only for a larger frame or another camera
+        if (m_batch) svo_align_batch_destroy(m_batch);
+        m_batch = nullptr;
+        const int32_t cap = std::max(nr + nk, same_cam ? 2 * m_batchCap : 1);
+        check(svo_align_batch_create(m_ctx.get(), &cam, &m_params, 1, cap, &m_batch));
+        m_batchCap = cap;
+        m_batchCam = cam;
     }
-    svo_align_batch_destroy(b);
+    double err = 0.0;
+    check(svo_align_batch_set_pair(m_batch, 0, refFrame->m_imagePyramid.set(), 0, kf->m_imagePyramid.set(), 0,
+                                   curFrame->m_imagePyramid.set(), 0, refFrame->m_absPose.data(), kf->m_absPose.data(),
+                                   curFrame->m_absPose.data(), nr, nk, m_px.data(), m_br.data(), m_pt.data(),
+                                   m_hp.data()));
+    check(svo_align_batch_run(m_batch));
+    check(svo_align_batch_results(m_batch, curFrame->m_absPose.data(), &err, &m_status));
     return err;
 }
 

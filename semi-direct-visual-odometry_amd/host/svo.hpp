@@ -111,9 +111,15 @@ struct Frame {  // include/frame.hpp:70-208 (the members the alignment path read
 };
 
 // ImageAlignment (include/image_alignment.hpp:15-73)
+// medianMode: SVO_MEDIAN_REFERENCE (default) reproduces the reference's robust scale bit for bit.
+// The single-pair batch is kept and grown on demand (no device allocation per align() once warm).
 class ImageAlignment {
 public:
-    ImageAlignment(Context& ctx, uint32_t patchSize, int32_t minLevel, int32_t maxLevel, uint32_t numParameters);
+    ImageAlignment(Context& ctx, uint32_t patchSize, int32_t minLevel, int32_t maxLevel, uint32_t numParameters,
+                   int32_t medianMode = SVO_MEDIAN_REFERENCE);
+    ~ImageAlignment();
+    ImageAlignment(const ImageAlignment&) = delete;
+    ImageAlignment& operator=(const ImageAlignment&) = delete;
     double align(std::shared_ptr<Frame>& refFrame, std::shared_ptr<Frame>& curFrame);
     int32_t lastStatus() const { return m_status; }
 
@@ -121,6 +127,11 @@ private:
     Context& m_ctx;
     svo_align_params m_params;
     int32_t m_status = SVO_STATUS_FAILED;
+    svo_align_batch* m_batch = nullptr;
+    int32_t m_batchCap = 0;
+    svo_camera m_batchCam{};
+    std::vector<double> m_px, m_br, m_pt;
+    std::vector<uint8_t> m_hp;
 };
 
 // FeatureAlignment (include/feature_alignment.hpp:15-43)

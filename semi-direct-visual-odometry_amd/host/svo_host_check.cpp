@@ -18,6 +18,11 @@
 //                                  prints "counts matches trials", then "px X Y" per new cur feature;
 //                                  an optional REPS argument also times REPS more runs on fresh object
 //                                  graphs ("ms T": reprojectMap + addCandidateToFrame, average)
+//   svo_host_check align DATA.bin REF.raw KF.raw CUR.raw PATCH MINL MAXL MEDIAN
+//                                  ImageAlignment::align (GPU) twice on one object from the same initial
+//                                  cur pose (the second call reuses the object's batch); DATA.bin (doubles):
+//                                  fx fy cx cy W H, ref/kf/cur pose[7], n_ref n_kf, then per feature
+//                                  px[2] bearing[3] point[3] has_point; prints "err status pose[7]" per call
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -137,6 +142,50 @@ int main(int argc, char** argv) {
             std::printf("filters %zu\n", de.numberFilters());
             for (const auto& c : cands)
                 std::printf("cand %.17g %.17g %.17g\n", c.second->m_position[0], c.second->m_position[1], c.second->m_position[2]);
+            return 0;
+        }
+        if (mode == "align" && argc >= 10) {
+            std::ifstream f(argv[2], std::ios::binary);
+            f.seekg(0, std::ios::end);
+            const size_t bytes = (size_t)f.tellg();
+            f.seekg(0);
+            std::vector<double> v(bytes / sizeof(double));
+            f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)bytes);
+            size_t q = 0;
+            auto take = [&]() { return v.at(q++); };
+            const double fx = take(), fy = take(), cx = take(), cy = take();
+            const int w = (int)take(), h = (int)take();
+            Pose poses[3];
+            for (auto& p : poses)
+                for (double& x : p) x = take();
+            const int nref = (int)take(), nkf = (int)take();
+            const int patch = std::atoi(argv[6]), minl = std::atoi(argv[7]), maxl = std::atoi(argv[8]);
+            const int median = std::atoi(argv[9]);
+            const std::vector<uint8_t> rimg = read_raw(argv[3], (size_t)w * h), kimg = read_raw(argv[4], (size_t)w * h),
+                                       cimg = read_raw(argv[5], (size_t)w * h);
+            Context ctx(0);
+            auto cam = std::make_shared<PinholeCamera>(PinholeCamera{w, h, fx, fy, cx, cy});
+            auto kf = std::make_shared<Frame>(ctx, cam, kimg.data(), maxl + 1);
+            auto ref = std::make_shared<Frame>(ctx, cam, rimg.data(), maxl + 1, kf);
+            auto cur = std::make_shared<Frame>(ctx, cam, cimg.data(), maxl + 1, kf);
+            ref->m_absPose = poses[0];
+            kf->m_absPose = poses[1];
+            for (int i = 0; i < nref + nkf; ++i) {
+                const double ux = take(), uy = take();
+                auto feat = std::make_shared<Feature>(i < nref ? ref.get() : kf.get(), Vec2{ux, uy});
+                feat->m_bearingVec = {take(), take(), take()};
+                const Vec3 pos{take(), take(), take()};
+                if (take() != 0.0) feat->m_point = std::make_shared<Point>(Point{pos});
+                (i < nref ? ref : kf)->m_features.push_back(feat);
+            }
+            ImageAlignment align(ctx, (uint32_t)patch, minl, maxl, 6, median);
+            for (int call = 0; call < 2; ++call) {
+                cur->m_absPose = poses[2];
+                const double e = align.align(ref, cur);
+                std::printf("%.17g %d", e, align.lastStatus());
+                for (double x : cur->m_absPose) std::printf(" %.17g", x);
+                std::printf("\n");
+            }
             return 0;
         }
         if (mode == "map" && argc >= 6) {

@@ -193,10 +193,20 @@ def test_class_surface_align():
         fr = ref if i < s.n_ref else kf
         f = svo_amd.Feature(fr, s.px[i], bearing=s.bearing[i], point=svo_amd.Point(s.point[i]))
         fr.add_feature(f)
-    err = svo_amd.ImageAlignment(5, 0, 4).align(ref, cur)
-    pc, ec, stc, _ = oracle_align(s, 5, 0, 4, mode=1)
+    ia = svo_amd.ImageAlignment(5, 0, 4)  # default: the reference's median semantics
+    err = ia.align(ref, cur)
+    pc, ec, stc, _ = oracle_align(s, 5, 0, 4, mode=0)  # oracle mode 0 = the reference's nth_element
     assert np.abs(canon(cur.abs_pose) - canon(pc)).max() <= 1e-9
     assert abs(err - ec) <= 1e-9 * ec
+    # a second call reuses the object's batch and repeats the first exactly
+    first = cur.abs_pose.copy()
+    cur.abs_pose[:] = s.cur_init_pose
+    assert ia.align(ref, cur) == err and np.array_equal(cur.abs_pose, first)
+    # exact order statistics on request
+    cur.abs_pose[:] = s.cur_init_pose
+    svo_amd.ImageAlignment(5, 0, 4, median_mode=svo_amd.MEDIAN_EXACT).align(ref, cur)
+    px_, ex_, _, _ = oracle_align(s, 5, 0, 4, mode=1)
+    assert np.abs(canon(cur.abs_pose) - canon(px_)).max() <= 1e-9
     # ImagePyramid getters (src/image_pyramid.cpp:54-124)
     assert np.array_equal(ref.image_pyramid.get_base_image(), s.ref_img)
     assert ref.image_pyramid.get_image_size_at_level(4) == (78, 24)

@@ -32,4 +32,6 @@ names = ("pivot", "sweep", "crossing", "partners", "swaps/copy")
 for w, kind in enumerate(("round 1", "global rounds", "lds rounds")):
     ph = out[10 + 5 * w: 15 + 5 * w]
     print(f"{kind:14s} cycles per phase (both passes): " + ", ".join(f"{n} {v:.0f}" for n, v in zip(names, ph)))
+ph = out[25:30]
+print("wave rounds    cycles per phase (both passes): " + ", ".join(f"{n} {v:.0f}" for n, v in zip(("pivot", "sweep", "crossing", "partners", "swaps"), ph)))
 print(f"exact classifications: pass 0 {out[30]:.0f}, pass 1 {out[31]:.0f}")
