@@ -108,6 +108,13 @@ def project2d(cam, p3):
     return out
 
 
+def inverse_project2d(cam, uv):
+    out = np.zeros(3)
+    uv = np.ascontiguousarray(uv, dtype=np.float64)
+    lib().oracle_inverse_project2d(ctypes.byref(camera(cam)), _p(uv), _p(out))
+    return out
+
+
 def se3_exp(tangent):
     t = np.ascontiguousarray(tangent, dtype=np.float64)
     out = np.zeros(7)

@@ -974,6 +974,15 @@ void oracle_project2d(const oc_camera* c, const double* p3, double* out2) {
     out2[1] = uv.y;
 }
 
+// PinholeCamera::inverseProject2d (src/pinhole_camera.cpp:81-101, no distortion): the unit bearing
+void oracle_inverse_project2d(const oc_camera* c, const double* uv, double* out3) {
+    Camera cam{c->fx, c->fy, c->cx, c->cy, c->width, c->height};
+    const V3 b = cam.inverse_project2d(uv[0], uv[1]);
+    out3[0] = b.x;
+    out3[1] = b.y;
+    out3[2] = b.z;
+}
+
 void oracle_se3_exp(const double* tangent6, double* out7) {
     SE3 T = se3_exp(tangent6);
     out7[0] = T.q.x; out7[1] = T.q.y; out7[2] = T.q.z; out7[3] = T.q.w;

@@ -45,7 +45,8 @@ namespace {
 constexpr int kRT = 512;               // threads per pair
 constexpr int kRW = kRT / 64;          // waves
 constexpr int kMeta = 1024;            // LDS step records (64 positions each): segments up to 65536
-constexpr int kBatch = 4;              // loads a lane issues before using any (copies, swaps)
+constexpr int kBatch = 4;
+constexpr uint32_t kWaveSteps = 8;     // segments of <= 8 steps run on one wave (block rounds above)              // loads a lane issues before using any (copies, swaps)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr double kDblMax = 1.7976931348623157e308;
 
@@ -78,6 +79,8 @@ struct RefShared {
     uint32_t ks, cut_l, cut_r, l_ks;
     uint32_t bc_first, bc_last, bc_depth, bc_rec;
     El lo_el, fin[3];
+    uint32_t wlog[22][3];  // diagnostics: per wave round (both passes): steps, sweep cycles, round cycles
+    uint32_t nwlog;
     uint64_t stamp[32];  // diagnostics (svo_debug_robust_scale): per pass: cycles of round 1, of the rest,
                          // block rounds, wave rounds; [8..] cycles per phase of block rounds; [28..] exact calls
 };
@@ -347,9 +350,13 @@ struct RefSel {
         } else if (less(src, P, med, a, c)) { ch = A; e = a; }
         else if (less(src, P, med, b, c)) { ch = C; e = c; }
         else { ch = B; e = b; }
-        pv.e = e;
         pv.f0 = get(first);
         pv.ch = ch;
+        pivot_fields(e);
+    }
+    // the pivot's pass-1 interval and key thresholds (uniform; every caller lane computes the same)
+    __device__ __forceinline__ void pivot_fields(El e) {
+        pv.e = e;
         pv.inv = e.key == kKeyInvisible;
         pv.plo = pv.phi = 0.0;
         pv.kA = pv.kB = pv.kC = pv.kD = 0;
@@ -382,17 +389,17 @@ struct RefSel {
     // holds the records of up to 64 RR steps in registers: lane j of row r = step s0 + 64 r + j.
     // Positions outside (first, last), `first` itself (the pivot: LE only) and ch (holding f0 after the
     // median-of-three swap) are fixed afterwards, per record (fix_rows).
-    template <int W>
-    __device__ __forceinline__ uint32_t load_key(uint32_t p) const {
-        if (W == kLds) return sh.key[p - base];
-        if (W == kGlb) return gkey[p];
-        return Src::key_at(kb, p);
+    // G: the segment is in global memory (gk = the read-only round-1 keys or the pair's scratch), else LDS.
+    // One instantiation serves both global kinds: code size is what limits the serial parts (I-cache).
+    template <bool G>
+    __device__ __forceinline__ uint32_t load_key(const uint32_t* gk, uint32_t p) const {
+        if (G) return gk[p];
+        return sh.key[p - base];
     }
-    template <int W>
+    template <bool G>
     __device__ __forceinline__ uint32_t load_id(uint32_t p) const {
-        if (W == kLds) return (uint32_t)sh.id[p - base];
-        if (W == kGlb) return gid[p];
-        return p;
+        if (G) return where == kSrc ? p : gid[p];
+        return (uint32_t)sh.id[p - base];
     }
     // bits i with a <= sp + i < b
     static __device__ __forceinline__ uint64_t range_mask(uint32_t sp, uint32_t a, uint32_t b) {
@@ -400,22 +407,51 @@ struct RefSel {
         const uint32_t hi = b > sp ? (b - sp < 64u ? b - sp : 64u) : 0u;
         return low_mask(hi) & ~low_mask(lo);
     }
-    template <int W>
+    template <bool G>
     __device__ __forceinline__ void slow_fix(uint32_t sp, uint32_t k, uint64_t sl, uint64_t& ge, uint64_t& le) const {
         sl &= range_mask(sp, first + 1, last);
         const bool me = (sl >> lane) & 1ull;
         uint32_t c = 0;
-        if (me) c = classify_slow(src, P, med, k, load_id<W>(sp + (uint32_t)lane), pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
+        if (me) c = classify_slow(src, P, med, k, load_id<G>(sp + (uint32_t)lane), pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
         ge = (ge & ~sl) | __ballot(me && (c & 1u));
         le = (le & ~sl) | __ballot(me && (c & 2u));
     }
-    template <int RR, int W, int PP>
+    // a step's masks from the compares; sl = positions the keys cannot settle
+    struct Thr {
+        uint32_t pk, tA, tB, tC, tD;
+        bool pslow, pinv;
+    };
+    __device__ __forceinline__ Thr thresholds() const {
+        Thr t;
+        t.pk = uni(pv.e.key);
+        t.tA = uni(pv.tA); t.tB = uni(pv.tB); t.tC = uni(pv.tC); t.tD = uni(pv.tD);
+        t.pslow = (t.pk & 1u) && t.pk != kKeyInvisible;  // pass 0: equal keys need the exact values
+        t.pinv = uni(pv.inv) != 0;
+        return t;
+    }
+    template <int PP>
+    static __device__ __forceinline__ void step_masks(const Thr& t, uint32_t k, uint64_t& ge, uint64_t& le, uint64_t& sl) {
+        if (PP == 0) {
+            ge = __ballot(k >= t.pk);
+            le = __ballot(k <= t.pk);
+            sl = t.pslow ? __ballot(k == t.pk) : 0ull;
+        } else if (t.pinv) {  // pivot DBL_MAX: every visible slot is less, DBL_MAX equal
+            ge = __ballot(k == kKeyInvisible);
+            le = ~0ull;
+            sl = 0ull;
+        } else {
+            const uint64_t lt = __ballot(k >= t.tA) & __ballot(k <= t.tB);
+            const uint64_t gt = __ballot(k <= t.tC) | __ballot(k >= t.tD);
+            ge = ~lt;
+            le = ~gt;
+            sl = ~(lt | gt);
+        }
+    }
+    template <int RR, bool G, int PP>
     __device__ __forceinline__ void sweep_rows(uint32_t b0, uint32_t s0, uint32_t n, uint64_t (&mg)[RR], uint64_t (&ml)[RR]) const {
-        const uint32_t pk = __builtin_amdgcn_readfirstlane(pv.e.key);
-        const uint32_t tA = __builtin_amdgcn_readfirstlane(pv.tA), tB = __builtin_amdgcn_readfirstlane(pv.tB);
-        const uint32_t tC = __builtin_amdgcn_readfirstlane(pv.tC), tD = __builtin_amdgcn_readfirstlane(pv.tD);
-        const bool pslow = (pk & 1u) && pk != kKeyInvisible;  // pass 0: equal keys need the exact values
-        const bool pinv = __builtin_amdgcn_readfirstlane(pv.inv) != 0;
+        b0 = uni(b0); s0 = uni(s0); n = uni(n);  // scalar loop control (see uni)
+        const uint32_t* const gk = where == kSrc ? kb : gkey;
+        const Thr t = thresholds();
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
             uint32_t g0 = 0, g1 = 0, l0 = 0, l1 = 0;
@@ -424,33 +460,36 @@ struct RefSel {
             for (uint32_t j0 = 0; j0 < nr; j0 += 8) {
                 uint32_t kv[8];
 #pragma unroll
-                for (int b = 0; b < 8; ++b) kv[b] = load_key<W>(b0 + 64u * (sr + j0 + (uint32_t)b) + (uint32_t)lane);
+                for (int b = 0; b < 8; ++b) kv[b] = load_key<G>(gk, b0 + 64u * (sr + j0 + (uint32_t)b) + (uint32_t)lane);
+                uint64_t any = 0;
 #pragma unroll
                 for (int b = 0; b < 8; ++b) {
                     const uint32_t j = j0 + (uint32_t)b;
                     if (j >= nr) break;  // wave-uniform
-                    const uint32_t k = kv[b];
                     uint64_t ge, le, sl;
-                    if (PP == 0) {
-                        ge = __ballot(k >= pk);
-                        le = __ballot(k <= pk);
-                        sl = pslow ? __ballot(k == pk) : 0ull;
-                    } else if (pinv) {  // pivot DBL_MAX: every visible slot is less, DBL_MAX equal
-                        ge = __ballot(k == kKeyInvisible);
-                        le = ~0ull;
-                        sl = 0ull;
-                    } else {
-                        const uint64_t lt = __ballot(k >= tA) & __ballot(k <= tB);
-                        const uint64_t gt = __ballot(k <= tC) | __ballot(k >= tD);
-                        ge = ~lt;
-                        le = ~gt;
-                        sl = ~(lt | gt);
-                    }
-                    if (sl) slow_fix<W>(b0 + 64u * (sr + j), k, sl, ge, le);
+                    step_masks<PP>(t, kv[b], ge, le, sl);
+                    any |= sl;
                     g0 = lane_write(g0, (uint32_t)ge, j);
                     g1 = lane_write(g1, (uint32_t)(ge >> 32), j);
                     l0 = lane_write(l0, (uint32_t)le, j);
                     l1 = lane_write(l1, (uint32_t)(le >> 32), j);
+                }
+                if (any) {  // rare: redo the batch's unsettled steps exactly (one copy of the slow path)
+                    const uint32_t je = j0 + 8u < nr ? j0 + 8u : nr;
+#pragma unroll 1
+                    for (uint32_t j = j0; j < je; ++j) {
+                        const uint32_t sp = b0 + 64u * (sr + j);
+                        const uint32_t k = load_key<G>(gk, sp + (uint32_t)lane);
+                        uint64_t ge, le, sl;
+                        step_masks<PP>(t, k, ge, le, sl);
+                        if (sl) {
+                            slow_fix<G>(sp, k, sl, ge, le);
+                            g0 = lane_write(g0, (uint32_t)ge, j);
+                            g1 = lane_write(g1, (uint32_t)(ge >> 32), j);
+                            l0 = lane_write(l0, (uint32_t)le, j);
+                            l1 = lane_write(l1, (uint32_t)(le >> 32), j);
+                        }
+                    }
                 }
             }
             mg[r] = ((uint64_t)g1 << 32) | g0;
@@ -460,13 +499,11 @@ struct RefSel {
     template <int RR>
     __device__ __forceinline__ void sweep_rows(uint32_t b0, uint32_t s0, uint32_t n, uint64_t (&mg)[RR], uint64_t (&ml)[RR]) const {
         if (P == 0) {
-            if (where == kLds) sweep_rows<RR, kLds, 0>(b0, s0, n, mg, ml);
-            else if (where == kGlb) sweep_rows<RR, kGlb, 0>(b0, s0, n, mg, ml);
-            else sweep_rows<RR, kSrc, 0>(b0, s0, n, mg, ml);
+            if (where == kLds) sweep_rows<RR, false, 0>(b0, s0, n, mg, ml);
+            else sweep_rows<RR, true, 0>(b0, s0, n, mg, ml);
         } else {
-            if (where == kLds) sweep_rows<RR, kLds, 1>(b0, s0, n, mg, ml);
-            else if (where == kGlb) sweep_rows<RR, kGlb, 1>(b0, s0, n, mg, ml);
-            else sweep_rows<RR, kSrc, 1>(b0, s0, n, mg, ml);
+            if (where == kLds) sweep_rows<RR, false, 1>(b0, s0, n, mg, ml);
+            else sweep_rows<RR, true, 1>(b0, s0, n, mg, ml);
         }
     }
     // the records' edge fixes (lanes holding a step of this wave only): GE in (first, last), LE in
@@ -499,40 +536,56 @@ struct RefSel {
     // R_k; k <= Ks go to the lists, L_{Ks+1} / L_{Ks} / R_{Ks} to the shared scalars (one position holds
     // each rank, so one lane writes each).  A step whose ranks all exceed Ks + 1 is skipped (uniform test):
     // left of the crossing only the GE part runs, right of it only the LE part.
-    template <int RR>
-    __device__ __forceinline__ void partners(uint32_t b0, uint32_t s0, uint32_t n, uint32_t ks, const uint64_t (&mg)[RR],
-                                             const uint64_t (&ml)[RR], const uint32_t (&gp)[RR], const uint32_t (&ls)[RR],
-                                             bool lds_lists) {
+    template <int RR, bool LL>
+    __device__ __forceinline__ void partners_t(uint32_t b0, uint32_t s0, uint32_t n, uint32_t ks, const uint64_t (&mg)[RR],
+                                               const uint64_t (&ml)[RR], const uint32_t (&gp)[RR], const uint32_t (&ls)[RR],
+                                               uint16_t* lpl, uint16_t* rpl) {
+        b0 = uni(b0); s0 = uni(s0); n = uni(n); ks = uni(ks);
         const uint64_t mybit = 1ull << lane;
+        auto put_l = [&](uint32_t k, uint32_t pos) {
+            if (LL) lpl[k - 1] = (uint16_t)(pos - b0);
+            else glp[k - 1] = pos;
+        };
+        auto put_r = [&](uint32_t k, uint32_t pos) {
+            if (LL) rpl[k - 1] = (uint16_t)(pos - b0);
+            else grp[k - 1] = pos;
+        };
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
             const uint32_t nr = n > 64u * r ? (n - 64u * r < 64u ? n - 64u * r : 64u) : 0u;
             for (uint32_t j = 0; j < nr; ++j) {
                 const uint32_t g = lane_read(gp[r], (int)j), l = lane_read(ls[r], (int)j);
                 const uint32_t pos = b0 + 64u * (s0 + 64u * r + j) + (uint32_t)lane;
-                if (g <= ks) {
+                if (g <= ks) {  // GE ranks g + 1 .. g + popc(a) reach Ks + 1
                     const uint64_t a = lane_read_u64(mg[r], (int)j);
-                    if (a & mybit) {
-                        const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(a >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a, g + 1u));
-                        if (k <= ks) {
-                            if (lds_lists) sh.lp[k - 1] = (uint16_t)(pos - b0);
-                            else glp[k - 1] = pos;
-                        }
+                    const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(a >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a, g + 1u));
+                    if (g + (uint32_t)__popcll(a) < ks) {  // every rank < Ks: plain compaction
+                        if (a & mybit) put_l(k, pos);
+                    } else if (a & mybit) {
+                        if (k <= ks) put_l(k, pos);
                         if (k == ks + 1u) sh.cut_l = pos;
                         if (k == ks) sh.l_ks = pos;
                     }
                 }
                 const uint64_t bb = lane_read_u64(ml[r], (int)j);
-                if (l - (uint32_t)__popcll(bb) < ks && (bb & mybit)) {
+                if (l - (uint32_t)__popcll(bb) < ks) {  // LE right-ranks l - popc + 1 .. l reach Ks
                     const uint32_t k = l - lanes_below(bb);
-                    if (k <= ks) {
-                        if (lds_lists) sh.rp[k - 1] = (uint16_t)(pos - b0);
-                        else grp[k - 1] = pos;
+                    if (l < ks) {
+                        if (bb & mybit) put_r(k, pos);
+                    } else if ((bb & mybit) && k <= ks) {
+                        put_r(k, pos);
                         if (k == ks) sh.cut_r = pos;
                     }
                 }
             }
         }
+    }
+    template <int RR>
+    __device__ __forceinline__ void partners(uint32_t b0, uint32_t s0, uint32_t n, uint32_t ks, const uint64_t (&mg)[RR],
+                                             const uint64_t (&ml)[RR], const uint32_t (&gp)[RR], const uint32_t (&ls)[RR],
+                                             bool lds_lists, uint16_t* lpl, uint16_t* rpl) {
+        if (lds_lists) partners_t<RR, true>(b0, s0, n, ks, mg, ml, gp, ls, lpl, rpl);
+        else partners_t<RR, false>(b0, s0, n, ks, mg, ml, gp, ls, lpl, rpl);
     }
 
     // ---------------------------------------------------------------- one block round (large segments)
@@ -542,6 +595,7 @@ struct RefSel {
     // and finds the crossing; barriers after the pivot, the sweep, the crossing, the partner lists and the
     // swaps.
     __device__ __forceinline__ void round() {
+        first = uni(first); last = uni(last);
         const uint32_t b0 = first & ~63u, ns = (last - b0 + 63) / 64;
         const uint32_t spw = (ns + kRW - 1) / kRW;
         uint64_t* const mge = R <= 2 ? sh.mge : gmge;
@@ -635,19 +689,24 @@ struct RefSel {
         phase(2);
         const uint32_t ks = uni(sh.ks);
         // ---- the swap partners of the wave's steps
-        const bool lds_lists = where == kLds;
+        // the lists: LDS segments keep them beside the segment; with 16-bit positions, a segment in global
+        // memory keeps them in the (then idle) LDS segment area, 32768 entries each (Ks <= S / 2 <= 32768)
+        const bool big = sizeof(Id) == 2 && where != kLds;
+        uint16_t* const lpl = big ? reinterpret_cast<uint16_t*>(sh.key) : sh.lp;
+        uint16_t* const rpl = big ? reinterpret_cast<uint16_t*>(sh.key) + 32768 : sh.rp;
+        const bool lds_lists = where == kLds || big;
         uint32_t gpr[R], lsr[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) { gpr[r] = gb + gex[r]; lsr[r] = lt - lb - lex[r]; }
-        partners<R>(b0, ws0, wsn, ks, mg, ml, gpr, lsr, lds_lists);
+        partners<R>(b0, ws0, wsn, ks, mg, ml, gpr, lsr, lds_lists, lpl, rpl);
         __syncthreads();
         phase(3);
         const uint32_t cut_l = uni(sh.cut_l), cut_r = ks > 0 ? uni(sh.cut_r) : kNone;
         const uint32_t cut = cut_l < cut_r ? cut_l : cut_r;
         const bool right = cut <= nth;  // the side introselect continues with
         const uint32_t nf = right ? cut : first, nl = right ? last : cut;
-        auto lpos = [&](uint32_t k) { return lds_lists ? b0 + sh.lp[k] : glp[k]; };  // L_{k+1}
-        auto rpos = [&](uint32_t k) { return lds_lists ? b0 + sh.rp[k] : grp[k]; };  // R_{k+1}
+        auto lpos = [&](uint32_t k) { return lds_lists ? b0 + lpl[k] : glp[k]; };  // L_{k+1}
+        auto rpos = [&](uint32_t k) { return lds_lists ? b0 + rpl[k] : grp[k]; };  // R_{k+1}
         // ---- vec[nth - 1] after this partition, if this cut leaves it behind for good
         if (cut == nth && !rec) {
             lo_el = (ks > 0 && sh.l_ks == cut - 1) ? elp(cut_r) : elp(cut - 1);
@@ -657,7 +716,9 @@ struct RefSel {
             // ---- copy the surviving side out of the read-only keys (coalesced), then the swap targets take
             // their partners
             uint32_t nb = nf & ~63u;
-            const int dst = (nl - nb) <= (uint32_t)kCap && M <= (sizeof(Id) == 2 ? 65536u : 0xFFFFFFFFu) ? kLds : kGlb;
+            // (16-bit positions: the lists occupy the LDS segment area, so the survivors go to global memory
+            // and move to LDS at the next round)
+            const int dst = !big && (nl - nb) <= (uint32_t)kCap && M <= (sizeof(Id) == 2 ? 65536u : 0xFFFFFFFFu) ? kLds : kGlb;
             if (dst == kGlb) nb = 0;
             const uint32_t n = nl - nf;
             for (uint32_t i0 = (uint32_t)tid; i0 < n; i0 += kRT * 8) {
@@ -743,20 +804,31 @@ struct RefSel {
     // LDS accesses of one wave complete in program order, so a lane reads what another lane wrote in an
     // earlier instruction.
     __device__ __forceinline__ void wave_round() {
+        first = uni(first); last = uni(last);
         const uint32_t b0 = first & ~63u, ns = (last - b0 + 63) / 64;
         uint64_t tp = clock64();
+        const uint64_t t_start = tp;
+        uint32_t t_sweep = 0;
         auto phase = [&](int i) {  // diagnostics: cycles per phase of the wave rounds
-            if (lane == 0) { const uint64_t t = clock64(); sh.stamp[23 + i] += t - tp; tp = t; }
+            if (lane == 0) {
+                const uint64_t t = clock64();
+                sh.stamp[23 + i] += t - tp;
+                if (i == 1) t_sweep = (uint32_t)(t - tp);
+                if (i == 4 && sh.nwlog < 22) {
+                    sh.wlog[sh.nwlog][0] = ns; sh.wlog[sh.nwlog][1] = t_sweep; sh.wlog[sh.nwlog][2] = (uint32_t)(t - t_start);
+                    sh.nwlog = sh.nwlog + 1;
+                }
+                tp = t;
+            }
         };
         choose_pivot();
         pv = uni(pv);
         if (lane == 0) { sh.cut_l = kNone; sh.cut_r = kNone; sh.l_ks = kNone; }
         const uint32_t f0c = classify(pv.f0.key, pv.ch);
-        uint64_t mg[1], ml[1];
+        uint64_t mg[R], ml[R];  // row 0 only (ns <= 64): the block round's instantiations, no extra code
         phase(0);
-        if (P == 0) sweep_rows<1, kLds, 0>(b0, 0, ns, mg, ml);
-        else sweep_rows<1, kLds, 1>(b0, 0, ns, mg, ml);
-        fix_rows<1>(b0, 0, ns, f0c, mg, ml);
+        sweep_rows<R>(b0, 0, ns, mg, ml);
+        fix_rows<R>(b0, 0, ns, f0c, mg, ml);
         phase(1);
         const uint32_t cg = (uint32_t)__popcll(mg[0]), cl = (uint32_t)__popcll(ml[0]);
         const uint32_t gi = wave_incl_scan(cg), li = wave_incl_scan(cl);
@@ -779,9 +851,11 @@ struct RefSel {
         const uint32_t ks = g1 > l2 ? g1 : l2;
         // ---- partners (lists in LDS) and L_{Ks+1}, L_{Ks}, R_{Ks}
         {
-            const uint32_t gpr[1] = {gpre}, lsr[1] = {lsuf};
+            uint32_t gpr[R], lsr[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) { gpr[r] = gpre; lsr[r] = lsuf; }
             phase(2);
-            partners<1>(b0, 0, ns, ks, mg, ml, gpr, lsr, true);
+            partners<R>(b0, 0, ns, ks, mg, ml, gpr, lsr, true, sh.lp, sh.rp);
         }
         const uint32_t cut_l = __builtin_amdgcn_readfirstlane(sh.cut_l);
         phase(3);
@@ -825,6 +899,87 @@ struct RefSel {
         last = nl;
     }
 
+    // ---------------------------------------------------------------- rounds of a segment of <= 64 elements
+    // One wave, lane = position - first, the elements in registers: the median of three by readlane, the
+    // masks by compares (as step_masks, restricted to the segment), Ks = max_t min(G(t), Lc(t)) by a wave max,
+    // each swap partner by a bit select on the masks, the swaps by ds_bpermute; vec[nth - 1] recorded from
+    // registers; the segment goes back to LDS once at the end.  Stops at <= 3 elements or depth 0.
+    __device__ __forceinline__ void lane_rounds(uint32_t& nrounds) {
+        first = uni(first); last = uni(last);
+        const uint32_t S0 = last - first, base0 = first;
+        const uint32_t me = (uint32_t)lane;
+        El e = me < S0 ? get(base0 + me) : El{kKeyInvisible, 0u};
+        uint32_t f = 0, l = S0;  // the segment, relative to base0
+        const uint32_t nrel = nth - base0;
+        const uint64_t below = low_mask(me);
+        while (l - f > 3 && depth > 0) {
+            --depth;
+            ++nrounds;
+            const uint32_t A = f + 1, B = f + (l - f) / 2, C = l - 1;
+            const El a{lane_read(e.key, (int)A), lane_read(e.id, (int)A)};
+            const El b{lane_read(e.key, (int)B), lane_read(e.id, (int)B)};
+            const El c{lane_read(e.key, (int)C), lane_read(e.id, (int)C)};
+            uint32_t ch;
+            El pe;
+            if (less(src, P, med, a, b)) {
+                if (less(src, P, med, b, c)) { ch = B; pe = b; }
+                else if (less(src, P, med, a, c)) { ch = C; pe = c; }
+                else { ch = A; pe = a; }
+            } else if (less(src, P, med, a, c)) { ch = A; pe = a; }
+            else if (less(src, P, med, b, c)) { ch = C; pe = c; }
+            else { ch = B; pe = b; }
+            const El f0{lane_read(e.key, (int)f), lane_read(e.id, (int)f)};
+            pivot_fields(uni(pe));
+            pv = uni(pv);
+            // the median-of-three swap (first <-> ch), then the masks over the segment
+            if (me == f) e = pv.e;
+            else if (me == ch) e = f0;
+            const Thr t = thresholds();
+            uint64_t ge, le, sl;
+            if (P == 0) step_masks<0>(t, e.key, ge, le, sl);
+            else step_masks<1>(t, e.key, ge, le, sl);
+            const uint64_t in_ge = low_mask(l) & ~low_mask(f + 1), in_le = low_mask(l) & ~low_mask(f);
+            sl &= in_ge;
+            if (sl) {
+                const bool mine = (sl >> me) & 1ull;
+                uint32_t cc = 0;
+                if (mine) cc = classify_slow(src, P, med, e.key, e.id, pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
+                ge = (ge & ~sl) | __ballot(mine && (cc & 1u));
+                le = (le & ~sl) | __ballot(mine && (cc & 2u));
+            }
+            ge &= in_ge;
+            le = (le & in_le) | (1ull << f);
+            // Ks: split t in [f+1, l) (t = l adds min(G, 0) = 0)
+            const uint32_t G = (uint32_t)__popcll(ge & below), Lc = (uint32_t)__popcll(le & ~below);
+            const uint32_t mm = (me >= f + 1 && me < l) ? (G < Lc ? G : Lc) : 0u;
+            const uint32_t ks = wave_max_u(mm);
+            // ranks: L_k = k-th GE from the left, R_k = k-th LE from the right
+            const bool isg = (ge >> me) & 1ull, isl = (le >> me) & 1ull;
+            const uint32_t kg = G + 1u, kl = Lc;  // this lane's GE rank / LE right-rank (when set)
+            const uint32_t cg = (uint32_t)__popcll(ge);
+            // L_{Ks+1} and R_{Ks} (kNone when absent), L_{Ks}
+            const uint32_t cut_l = ks + 1u <= cg ? wave_min_u(isg && kg == ks + 1u ? me : kNone) : kNone;
+            const uint32_t cut_r = ks > 0 ? wave_min_u(isl && kl == ks ? me : kNone) : kNone;
+            const uint32_t cut = cut_l < cut_r ? cut_l : cut_r;
+            // swap partners: the L_k lane takes R_k, the R_k lane takes L_k (k <= Ks)
+            uint32_t src_lane = me;
+            if (isg && kg <= ks) src_lane = 63u - select_bit(__builtin_bitreverse64(le), kg - 1u);
+            if (isl && kl <= ks) src_lane = select_bit(ge, kl - 1u);
+            const El ne{(uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4u), (int)e.key),
+                        (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane * 4u), (int)e.id)};
+            e = ne;
+            const bool right = cut <= nrel;
+            if (cut == nrel && !rec && nrel >= 1) lo_el = El{lane_read(e.key, (int)(cut - 1)), lane_read(e.id, (int)(cut - 1))};
+            rec = rec || cut == nrel;
+            if (right) f = cut;
+            else l = cut;
+        }
+        if (me < S0) put(base0 + me, e);
+        __builtin_amdgcn_wave_barrier();
+        first = base0 + f;
+        last = base0 + l;
+    }
+
     // ---------------------------------------------------------------- std::nth_element(vec, vec + nth)
     // (vec[nth - 1], vec[nth]) of the post-state as values (lo only when nth >= 1), on thread 0
     __device__ __forceinline__ void select(double& lo, double& hi) {
@@ -841,9 +996,13 @@ struct RefSel {
                 __syncthreads();
                 break;
             }
-            if (where == kLds && last - (first & ~63u) <= 64u * 64u) {  // the rest by wave 0, no barriers
+            if (where == kLds && last - (first & ~63u) <= 64u * kWaveSteps) {  // the rest by wave 0, no barriers
                 if (wave == 0) {
                     while (last - first > 3 && depth > 0) {
+                        if (last - first <= 64u) {
+                            lane_rounds(nwave);
+                            break;
+                        }
                         --depth;
                         wave_round();
                         ++nwave;
@@ -1010,6 +1169,7 @@ __global__ void __launch_bounds__(kRT, 1) debug_robust_scale_kernel(const double
                                                                    int flags) {
     __shared__ RefShared<Id> sh;
     if (threadIdx.x < 32) sh.stamp[threadIdx.x] = 0;
+    if (threadIdx.x == 0) sh.nwlog = 0;
     (void)flags;
     // the keys K1 would have written (res_key32), into the tail of the scratch
     const int64_t q = sel_stride / 4;
@@ -1024,6 +1184,7 @@ __global__ void __launch_bounds__(kRT, 1) debug_robust_scale_kernel(const double
         out[0] = med;
         out[1] = mad;
         for (int i = 0; i < 30; ++i) out[2 + i] = (double)sh.stamp[i];
+        for (int i = 0; i < 66; ++i) out[32 + i] = i / 3 < (int)sh.nwlog ? (double)sh.wlog[i / 3][i % 3] : -1.0;
     }
 }
 

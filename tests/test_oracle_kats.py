@@ -183,3 +183,30 @@ def test_oracle_robust_scale_on_flat_blocks():
         s = synth.make_flat_blocks(groups)
         _, _, _, tr = oracle_align(s, 5, 0, 0, mode=1)
         assert (tr[0].n_vis, tr[0].median, tr[0].mad) == (25 * sum(groups.values()), med, mad)
+
+
+def test_image_jac_vs_reference_sympy():
+    """The oracle's 2x6 image Jacobian against the reference's own sympy derivation (python/symbol.py:50-60,
+    `final = first * second`, lambdified by tests/golden/make_golden_symbol.py into symbol_jac.npz) and the
+    reference formula (src/image_alignment.cpp:235-247): equal to within 2 ulp (sympy's expression tree
+    orders some products differently: fx + fx*x**2/z2 vs (fx*x2)/z2 + fx)."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "symbol_jac.npz"))
+    for (fx, fy, x, y, z), ref in zip(d["inputs"], d["jac"]):
+        got = O.image_jac([x, y, z], fx, fy)
+        assert got[0, 1] == 0.0 and got[1, 0] == 0.0 and ref[0, 1] == 0.0 and ref[1, 0] == 0.0
+        scale = np.maximum(np.abs(ref), 1e-300)
+        assert (np.abs(got - ref) / scale).max() <= 2 * np.finfo(np.float64).eps, (fx, fy, x, y, z)
+
+
+def test_inverse_projection_round_trip():
+    """tests/test_camera.cpp:97-102: inverse projection of the projected KAT point recovers the point within
+    testMaxError = 1e-12 (:8).  The test is written against an older z-normalised invProject2d; the current
+    PinholeCamera::inverseProject2d (src/pinhole_camera.cpp:81-101) returns the unit bearing, so the point is
+    the bearing scaled by |P| (and the z-normalised form bearing / bearing.z * z)."""
+    cam = dict(fx=30.3, fy=40.4, cx=325.5, cy=248.8, width=640, height=480)
+    P = np.array([17.7, 28.8, 39.9])
+    b = O.inverse_project2d(cam, O.project2d(cam, P))
+    assert abs(np.linalg.norm(b) - 1.0) <= 1e-15
+    np.testing.assert_allclose(b * np.linalg.norm(P), P, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(b / b[2] * P[2], P, rtol=0, atol=1e-12)

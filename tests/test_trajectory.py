@@ -125,3 +125,15 @@ def test_errors_are_codes():
         import ctypes
         from svo_amd._capi import check, lib, ptr
         check(lib().svo_format_kitti_pose(ptr(p), ctypes.create_string_buffer(8), 8))
+
+
+@pytest.mark.gpu
+def test_trajectory_row_on_gpu_box():
+    """The same checks inside the GPU tier (the driver's -m gpu run on the MI355X box), so this §8(f) row is
+    exercised with the GPU build of libsvo_hip.so / svo_host_check as the box loads it."""
+    test_kitti_line_matches_oracle_stream()
+    test_matrix3x4_is_camera_to_world()
+    test_g6_matches_ostream()
+    test_cpp_mirror_writes_the_same_lines()
+    test_feature_dump_format_and_reader_quirk()
+    test_errors_are_codes()
