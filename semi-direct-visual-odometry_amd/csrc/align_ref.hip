@@ -81,6 +81,8 @@ struct RefShared {
     El lo_el, fin[3];
     uint32_t wlog[22][3];  // diagnostics: per wave round (both passes): steps, sweep cycles, round cycles
     uint32_t nwlog;
+    uint32_t blog[40][3];  // diagnostics: per block round: segment size, where, cycles
+    uint32_t nblog;
     uint64_t stamp[32];  // diagnostics (svo_debug_robust_scale): per pass: cycles of round 1, of the rest,
                          // block rounds, wave rounds; [8..] cycles per phase of block rounds; [28..] exact calls
 };
@@ -181,7 +183,7 @@ __device__ __attribute__((noinline)) uint32_t classify_slow(const Src* src, int 
         if (hi < plo) return 2u;
         if (lo > phi) return 1u;
     }
-    atomicAdd((unsigned long long*)counter, 1ull);  // diagnostics
+    if (counter) atomicAdd((unsigned long long*)counter, 1ull);  // diagnostics
     const double v = value(src, P, med, El{k, id}), p = value(src, P, med, pe);
     return (!(v < p) ? 1u : 0u) | (!(p < v) ? 2u : 0u);
 }
@@ -276,7 +278,8 @@ __device__ __forceinline__ Pivot uni(const Pivot& p) {
     return q;
 }
 
-template <class Src, typename Id>
+// kSt: diagnostics (svo_debug_robust_scale): clock stamps per phase / round; compiled out of the product
+template <class Src, typename Id, bool kSt>
 struct RefSel {
     using Shared = RefShared<Id>;
     static constexpr int kCap = Shared::kCap;
@@ -334,7 +337,7 @@ struct RefSel {
             // |r - med| > phi for the whole cell: r two grid steps outside [med - phi, med + phi]
             if (g <= pv.kC - 2 || g >= pv.kD + 2) return 1u;
         }
-        return classify_slow(src, P, med, k, idp(p), pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
+        return classify_slow(src, P, med, k, idp(p), pv.e, pv.plo, pv.phi, kSt ? &sh.stamp[28 + P] : nullptr);
     }
     // the pivot: std::__move_median_to_first(first, first + 1, first + S/2, last - 1) and the pass-1
     // interval / thresholds of the chosen element (uniform; every caller lane computes the same)
@@ -412,7 +415,7 @@ struct RefSel {
         sl &= range_mask(sp, first + 1, last);
         const bool me = (sl >> lane) & 1ull;
         uint32_t c = 0;
-        if (me) c = classify_slow(src, P, med, k, load_id<G>(sp + (uint32_t)lane), pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
+        if (me) c = classify_slow(src, P, med, k, load_id<G>(sp + (uint32_t)lane), pv.e, pv.plo, pv.phi, kSt ? &sh.stamp[28 + P] : nullptr);
         ge = (ge & ~sl) | __ballot(me && (c & 1u));
         le = (le & ~sl) | __ballot(me && (c & 2u));
     }
@@ -602,19 +605,14 @@ struct RefSel {
         uint64_t* const mle = R <= 2 ? sh.mle : gmle;
         uint32_t* const mgp = R <= 2 ? sh.gpre : ggpre;
         uint32_t* const mls = R <= 2 ? sh.lsuf : glsuf;
-        uint64_t tp = clock64();
+        uint64_t tp = kSt ? clock64() : 0;
         auto phase = [&](int i) {
-            if (tid == 0) { const uint64_t t = clock64(); sh.stamp[8 + 5 * where + i] += t - tp; tp = t; }
+            if (kSt && tid == 0) { const uint64_t t = clock64(); sh.stamp[8 + 5 * where + i] += t - tp; tp = t; }
         };
-        if (wave == 0) {
-            choose_pivot();
-            if (lane == 0) {
-                sh.piv = pv;
-                sh.cut_l = kNone; sh.cut_r = kNone; sh.l_ks = kNone;
-            }
-        }
-        __syncthreads();
-        pv = uni(sh.piv);
+        // every wave chooses the same pivot (3 reads and compares; no barrier, no broadcast)
+        choose_pivot();
+        pv = uni(pv);
+        if (tid == 0) { sh.cut_l = kNone; sh.cut_r = kNone; sh.l_ks = kNone; }  // read after two barriers
         phase(0);
         // ---- classification sweep of the wave's steps, records in registers, then to the step arrays
         const uint32_t ws0 = (uint32_t)wave * spw;
@@ -650,7 +648,8 @@ struct RefSel {
             const uint32_t j = 64 * (uint32_t)r + (uint32_t)lane;
             if (j < wsn) { mgp[ws0 + j] = gb + gex[r]; mls[ws0 + j] = lt - lb - lex[r]; }
         }
-        if (wave == 0) {
+        uint32_t ks;
+        {  // every wave finds the same crossing (no barrier, no broadcast)
             const uint32_t g_start = wgi - wg, l_start = lt - (wli - wl);
             const uint32_t wc = (uint32_t)__builtin_ctzll(__ballot(lane < kRW && g_start < l_start && g_start + wg >= l_start - wl));
             const uint32_t cs0 = wc * spw, csn = cs0 >= ns ? 0u : (ns - cs0 < spw ? ns - cs0 : spw);
@@ -682,12 +681,9 @@ struct RefSel {
             }
             const uint32_t g1 = gcar + (uint32_t)__popcll(a & low_mask(lo - 1));
             const uint32_t l2 = lcar - (uint32_t)__popcll(bb & low_mask(lo));
-            if (lane == 0) sh.ks = g1 > l2 ? g1 : l2;
+            ks = uni(g1 > l2 ? g1 : l2);
         }
-        if (R > 2) __threadfence_block();
-        __syncthreads();
         phase(2);
-        const uint32_t ks = uni(sh.ks);
         // ---- the swap partners of the wave's steps
         // the lists: LDS segments keep them beside the segment; with 16-bit positions, a segment in global
         // memory keeps them in the (then idle) LDS segment area, 32768 entries each (Ks <= S / 2 <= 32768)
@@ -806,11 +802,11 @@ struct RefSel {
     __device__ __forceinline__ void wave_round() {
         first = uni(first); last = uni(last);
         const uint32_t b0 = first & ~63u, ns = (last - b0 + 63) / 64;
-        uint64_t tp = clock64();
+        uint64_t tp = kSt ? clock64() : 0;
         const uint64_t t_start = tp;
         uint32_t t_sweep = 0;
         auto phase = [&](int i) {  // diagnostics: cycles per phase of the wave rounds
-            if (lane == 0) {
+            if (kSt && lane == 0) {
                 const uint64_t t = clock64();
                 sh.stamp[23 + i] += t - tp;
                 if (i == 1) t_sweep = (uint32_t)(t - tp);
@@ -943,7 +939,7 @@ struct RefSel {
             if (sl) {
                 const bool mine = (sl >> me) & 1ull;
                 uint32_t cc = 0;
-                if (mine) cc = classify_slow(src, P, med, e.key, e.id, pv.e, pv.plo, pv.phi, &sh.stamp[28 + P]);
+                if (mine) cc = classify_slow(src, P, med, e.key, e.id, pv.e, pv.plo, pv.phi, kSt ? &sh.stamp[28 + P] : nullptr);
                 ge = (ge & ~sl) | __ballot(mine && (cc & 1u));
                 le = (le & ~sl) | __ballot(mine && (cc & 2u));
             }
@@ -985,7 +981,7 @@ struct RefSel {
     __device__ __forceinline__ void select(double& lo, double& hi) {
         first = 0; last = M; base = 0; where = kSrc; rec = 0;
         depth = M > 1 ? 2 * lg2(M) : 0;
-        const uint64_t t0 = clock64();
+        const uint64_t t0 = kSt ? clock64() : 0;
         uint64_t t1 = t0;
         uint32_t nblk = 0, nwave = 0;
         while (last - first > 3) {
@@ -1029,15 +1025,25 @@ struct RefSel {
                 base = nb;
                 __syncthreads();
             }
-            round();
+            {
+                const uint64_t tb = kSt ? clock64() : 0;
+                const uint32_t S = last - first, w = (uint32_t)where;
+                round();
+                if (kSt && tid == 0 && sh.nblog < 40) {
+                    sh.blog[sh.nblog][0] = S; sh.blog[sh.nblog][1] = w; sh.blog[sh.nblog][2] = (uint32_t)(clock64() - tb);
+                    sh.nblog = sh.nblog + 1;
+                }
+            }
             ++nblk;
-            if (nblk == 1) t1 = clock64();
+            if (kSt && nblk == 1) t1 = clock64();
         }
-        if (tid == 0) {
+        if (kSt && tid == 0) {
             sh.stamp[4 * P] = t1 - t0;
             sh.stamp[4 * P + 1] = clock64() - t1;
             sh.stamp[4 * P + 2] = nblk;
             sh.stamp[4 * P + 3] = nwave;
+        }
+        if (tid == 0) {
             if (last - first <= 3) {  // std::__insertion_sort of the last <= 3
                 const uint32_t n = last - first;
                 El v[3];
@@ -1061,14 +1067,14 @@ struct RefSel {
 
 // computeMedian / computeMAD (src/algorithm.cpp:834-865) with the reference's post-state: thread 0 of the
 // block gets med and mad.  M slots, n visible.
-template <typename Id, class Src>
+template <typename Id, bool kSt, class Src>
 __device__ __forceinline__ void ref_robust_scale(const Src& src, RefShared<Id>& sh, uint32_t* sel, int64_t sel_stride,
                                                  uint32_t M, uint32_t n, double& med, double& mad) {
     const int tid = (int)threadIdx.x;
     __shared__ Src src_sh;
     if (tid == 0) src_sh = src;
     __syncthreads();
-    RefSel<Src, Id> s{&src_sh, sh};
+    RefSel<Src, Id, kSt> s{&src_sh, sh};
     s.kb = src.kbase();
     const int64_t q = sel_stride / 4;  // q >= M entries each: keys, ids, step records, partner lists
     s.gkey = sel;
@@ -1138,7 +1144,7 @@ __device__ __forceinline__ void scale_ref_pair(const AlignArgs& a, int level, Re
         src.half = a.half;
         src.n_ref = P.n_ref;
         src.scale = ldexp(1.0, -level);
-        ref_robust_scale<Id>(src, sh, a.sel + (int64_t)pair * a.sel_stride, a.sel_stride, M, n, med, mad);
+        ref_robust_scale<Id, false>(src, sh, a.sel + (int64_t)pair * a.sel_stride, a.sel_stride, M, n, med, mad);
     }
     if (tid == 0) {
         double sigma = 1.482602218505602 * mad;
@@ -1169,7 +1175,7 @@ __global__ void __launch_bounds__(kRT, 1) debug_robust_scale_kernel(const double
                                                                    int flags) {
     __shared__ RefShared<Id> sh;
     if (threadIdx.x < 32) sh.stamp[threadIdx.x] = 0;
-    if (threadIdx.x == 0) sh.nwlog = 0;
+    if (threadIdx.x == 0) { sh.nwlog = 0; sh.nblog = 0; }
     (void)flags;
     // the keys K1 would have written (res_key32), into the tail of the scratch
     const int64_t q = sel_stride / 4;
@@ -1179,12 +1185,13 @@ __global__ void __launch_bounds__(kRT, 1) debug_robust_scale_kernel(const double
     __syncthreads();
     ArrSrc src{v, keys};
     double med = 0.0, mad = 0.0;
-    ref_robust_scale<Id>(src, sh, sel, sel_stride, M, n, med, mad);
+    ref_robust_scale<Id, true>(src, sh, sel, sel_stride, M, n, med, mad);
     if (threadIdx.x == 0) {
         out[0] = med;
         out[1] = mad;
         for (int i = 0; i < 30; ++i) out[2 + i] = (double)sh.stamp[i];
         for (int i = 0; i < 66; ++i) out[32 + i] = i / 3 < (int)sh.nwlog ? (double)sh.wlog[i / 3][i % 3] : -1.0;
+        for (int i = 0; i < 120; ++i) out[98 + i] = i / 3 < (int)sh.nblog ? (double)sh.blog[i / 3][i % 3] : -1.0;
     }
 }
 

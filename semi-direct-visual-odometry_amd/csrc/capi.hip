@@ -737,7 +737,7 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
             return fail(SVO_ERR_ARG, "value %lld = %g outside [-255, 255] and not DBL_MAX", (long long)i, values[i]);
     SVO_HIP(hipSetDevice(c->device));
     const int64_t q = (n_slots + 63) / 64 * 64;
-    const size_t bytes = (size_t)q * 8 + (size_t)5 * q * 4 + 1024;
+    const size_t bytes = (size_t)q * 8 + (size_t)5 * q * 4 + 2048;
     void* base = nullptr;
     hipError_t e = ctx_scratch(c, bytes, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_debug_robust_scale: %s", hipGetErrorString(e));
@@ -750,7 +750,7 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
     svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, 4 * q, d_out,
                                    st && st[0] == '2' ? 1 : 0, c->stream);
     SVO_HIP(hipGetLastError());
-    SVO_HIP(hipMemcpyAsync(med_mad, d_out, getenv("SVO_DEBUG_STAMPS") ? 98 * 8 : 16, hipMemcpyDeviceToHost, c->stream));
+    SVO_HIP(hipMemcpyAsync(med_mad, d_out, getenv("SVO_DEBUG_STAMPS") ? 218 * 8 : 16, hipMemcpyDeviceToHost, c->stream));
     SVO_HIP(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }

@@ -17,7 +17,7 @@ v = rng.normal(0, 8, 50000)
 v[np.repeat(rng.random(2000) < 0.2, 25)] = np.finfo(np.float64).max
 n = int((v < 1e300).sum())
 ctx = svo_amd.default_context()
-out = np.zeros(98)
+out = np.zeros(218)
 for _ in range(3):
     _capi.check(_capi.lib().svo_debug_robust_scale(ctx.handle, _capi.ptr(v), len(v), n, _capi.ptr(out)))
 t0 = time.perf_counter()
@@ -37,3 +37,5 @@ print("wave rounds    cycles per phase (both passes): " + ", ".join(f"{n} {v:.0f
 print(f"exact classifications: pass 0 {out[30]:.0f}, pass 1 {out[31]:.0f}")
 wl = out[32:98].reshape(-1, 3)
 print("wave rounds (steps, sweep cycles, round cycles):", [tuple(int(x) for x in r) for r in wl if r[0] >= 0])
+bl = out[98:218].reshape(-1, 3)
+print("block rounds (S, where 0 src 1 glb 2 lds, cycles):", [tuple(int(x) for x in r) for r in bl if r[0] >= 0])
