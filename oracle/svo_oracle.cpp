@@ -37,6 +37,8 @@
 #include <sstream>
 #include <string>
 #include <limits>
+#include <pthread.h>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -1071,8 +1073,24 @@ void oracle_image_align_batch(const oc_camera* c, int32_t patch, int32_t min_lev
         }
     };
     if (nthreads <= 1) { worker(); return; }
+    // one worker per CPU of the process's affinity mask, each pinned to its CPU (the CPU baseline's
+    // "nproc pinned threads"); more threads than CPUs wrap around the mask
+    cpu_set_t mask;
+    CPU_ZERO(&mask);
+    std::vector<int> cpus;
+    if (sched_getaffinity(0, sizeof(mask), &mask) == 0)
+        for (int cpu = 0; cpu < CPU_SETSIZE; ++cpu)
+            if (CPU_ISSET(cpu, &mask)) cpus.push_back(cpu);
     std::vector<std::thread> th;
-    for (int32_t t = 0; t < nthreads; ++t) th.emplace_back(worker);
+    for (int32_t t = 0; t < nthreads; ++t) {
+        th.emplace_back(worker);
+        if (!cpus.empty()) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(cpus[(size_t)t % cpus.size()], &one);
+            (void)pthread_setaffinity_np(th.back().native_handle(), sizeof(one), &one);
+        }
+    }
     for (auto& t : th) t.join();
 }
 
