@@ -80,17 +80,19 @@ def test_gpu_matches_golden():
         for l, (hh, ww, off) in enumerate(O.level_shapes(c["width"], c["height"], 4)):
             assert np.array_equal(ps.download(i, l).ravel(), g[f"{k}_stack"][off:off + hh * ww])
             assert np.array_equal(ps.download(i, l, True).ravel(), g[f"{k}_grad"][off:off + hh * ww])
-    b = svo_amd.AlignBatch(camera, int(d["patch"]), 0, L - 1, 1, len(d["px"]))
-    b.set_pair(0, (ps, 0), (ps, 1), (ps, 2), d["ref_pose"], d["kf_pose"], d["cur_init_pose"], int(d["n_ref"]),
-               int(d["n_kf"]), d["px"], d["bearing"], d["point"], d["has_point"])
-    b.run()
-    pose, err, st = b.results()
-    assert np.abs(canon(pose[0]) - canon(d["m1_pose"])).max() <= 1e-9
-    assert np.abs(canon(pose[0]) - canon(d["m0_pose"])).max() <= 1e-5
-    assert abs(err[0] - d["m1_err"]) <= 1e-9 * d["m1_err"] and st[0] == d["m1_status"]
-    tr = b.traces(0)
-    assert [t.n_vis for t in tr] == list(d["m1_trace_n_vis"])
-    assert [t.n_ref_vis for t in tr] == list(d["m1_trace_n_ref_vis"])
+    # golden m0 = the reference's nth_element semantics (SVO_MEDIAN_REFERENCE), m1 = exact order statistics
+    for gpu_mode, m in ((svo_amd.MEDIAN_REFERENCE, "m0"), (svo_amd.MEDIAN_EXACT, "m1")):
+        b = svo_amd.AlignBatch(camera, int(d["patch"]), 0, L - 1, 1, len(d["px"]), median_mode=gpu_mode)
+        b.set_pair(0, (ps, 0), (ps, 1), (ps, 2), d["ref_pose"], d["kf_pose"], d["cur_init_pose"], int(d["n_ref"]),
+                   int(d["n_kf"]), d["px"], d["bearing"], d["point"], d["has_point"])
+        b.run()
+        pose, err, st = b.results()
+        assert np.abs(canon(pose[0]) - canon(d[f"{m}_pose"])).max() <= 1e-9
+        assert np.abs(canon(pose[0]) - canon(d["m0_pose"])).max() <= 1e-5
+        assert abs(err[0] - d[f"{m}_err"]) <= 1e-9 * d[f"{m}_err"] and st[0] == d[f"{m}_status"]
+        tr = b.traces(0)
+        assert [t.n_vis for t in tr] == list(d[f"{m}_trace_n_vis"])
+        assert [t.n_ref_vis for t in tr] == list(d[f"{m}_trace_n_ref_vis"])
     fd = load("feature_small.npz")
     ps2 = svo_amd.PyramidSet(2, c["width"], c["height"], 1)
     ps2.upload(0, np.stack([d["ref_img"], d["cur_img"]]))
