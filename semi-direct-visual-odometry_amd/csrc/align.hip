@@ -267,18 +267,21 @@ __device__ __forceinline__ V3 world_point(const AlignArgs& a, const PairDesc& P,
 // are formed once and shared by the two patch rows that read them: bit-identical to the per-sample
 // formula whenever x1 = floor(u) + kx and y1 = floor(v) + ky.  A feature where u + kx rounds up to the
 // next integer (x1 = floor(u) + kx + 1) takes the per-pixel path instead.
-// kRef (median_mode SVO_MEDIAN_REFERENCE): 32-bit keys (res_key32) in the reference's feature-major slot
-// order (slot f * area + k, the order K2R's introselect runs over) instead of 16-bit pixel-major ones.
+// kRef (median_mode SVO_MEDIAN_REFERENCE): the exact residuals (doubles, DBL_MAX for an invisible slot) in
+// the reference's feature-major slot order (slot f * area + k, the vector K2R's introselect runs over)
+// instead of 16-bit pixel-major keys.
 template <int kHalf, bool kWin, bool kRef>  // kWin: a window level (AlignArgs::win_levels)
 __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual_kernel(AlignArgs a, int level) {
     using G = Win<kHalf>;
-    using KeyT = typename std::conditional<kRef, uint32_t, uint16_t>::type;
+    using KeyT = typename std::conditional<kRef, double, uint16_t>::type;
     constexpr int h = G::h, side = G::side, RB = G::RB, NW = G::RW;
-    constexpr KeyT kInvis = kRef ? (KeyT)kKeyInvisible : (KeyT)0xFFFF;
+    constexpr KeyT kInvis = kRef ? (KeyT)1.7976931348623157e308 : (KeyT)0xFFFF;
     // keys are staged in LDS ([pixel][feature], or [feature][pixel] for kRef) and written as whole 16-B
     // pieces of the slot rows (one 2-B store per lane and pixel wrote each 128-B line in many partial
     // requests: 2.8x the key bytes)
-    constexpr bool kLds = G::A * kLaneFeats * (int)sizeof(KeyT) <= 32768;
+    // (kRef: the residual doubles are staged too, up to 64 KB: one 8-B store per lane and pixel at a
+    // 200-B lane stride touched 64 lines per instruction)
+    constexpr bool kLds = G::A * kLaneFeats * (int)sizeof(KeyT) <= (kRef ? 65536 : 32768);
     __shared__ __attribute__((aligned(16))) KeyT kbuf[kLds ? G::A * kLaneFeats : 1];
     int pair, chunk;
     xcd_pair_chunk(a.chunks, pair, chunk);
@@ -305,13 +308,13 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
             if constexpr (kRef) kbuf[tid * G::A + k] = key;
             else kbuf[k * kLaneFeats + tid] = key;
         } else if constexpr (kRef) {
-            a.keys32[(int64_t)pair * a.key_stride + (int64_t)f * G::A + k] = key;
+            a.scratch[(int64_t)pair * a.key_stride + (int64_t)f * G::A + k] = key;
         } else {
             slot_store16(keys, 2 * fo, 2 * (uint32_t)(k * fstride), key);
         }
     };
     auto rkey = [](double r) -> KeyT {
-        if constexpr (kRef) return res_key32(r);
+        if constexpr (kRef) return r;
         else return res_key(r);
     };
     int vis = 0;
@@ -429,9 +432,9 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
     if constexpr (kLds && kRef) {  // the workgroup's features are one contiguous run of slots
         __syncthreads();
         const int nfe = fstride - f0 < kLaneFeats ? fstride - f0 : kLaneFeats;  // a multiple of 64
-        uint32_t* const kp = a.keys32 + (int64_t)pair * a.key_stride + (int64_t)f0 * G::A;
-        for (int idx = tid; idx < nfe * G::A / 4; idx += kLaneFeats)
-            *reinterpret_cast<uint4*>(kp + 4 * idx) = *reinterpret_cast<const uint4*>(&kbuf[4 * idx]);
+        double* const kp = a.scratch + (int64_t)pair * a.key_stride + (int64_t)f0 * G::A;
+        for (int idx = tid; idx < nfe * G::A / 2; idx += kLaneFeats)
+            *reinterpret_cast<uint4*>(kp + 2 * idx) = *reinterpret_cast<const uint4*>(&kbuf[2 * idx]);
     } else if constexpr (kLds) {
         __syncthreads();
         const int per_row = (fstride - f0 < kLaneFeats ? fstride - f0 : kLaneFeats) / 8;  // 16-B pieces

@@ -144,7 +144,6 @@ struct svo_align_batch {
     int32_t n_pairs, max_f, half, area;
     int64_t key_stride;
     uint16_t* d_keys;
-    uint32_t* d_keys32;   // median_mode 1
     uint32_t* d_sel;      // median_mode 1: K2R scratch
     int64_t sel_stride;
     uint32_t* d_win;
@@ -332,7 +331,7 @@ int svo_pyramid_level_size(const svo_pyramid_set* p, int32_t level, int32_t* w, 
 
 // ------------------------------------------------------------------ image alignment batches
 static void free_batch(svo_align_batch* b) {
-    void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_keys, b->d_keys32, b->d_sel,
+    void* ptrs[] = {b->d_pairs, b->d_px, b->d_bearing, b->d_point, b->d_has_point, b->d_xw, b->d_keys, b->d_sel,
                     b->d_state, b->d_partials, b->d_arrive, b->d_fvis, b->d_cproj, b->d_scratch, b->d_pose_out, b->d_err, b->d_status, b->d_traces,
                     b->d_win, b->d_stage};
     for (void* p : ptrs)
@@ -384,9 +383,9 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     b->key_stride = slots;
     ALLOC(b->d_cproj, F * 2 * sizeof(double));
     if (prm->median_mode == SVO_MEDIAN_REFERENCE) {
-        // K2R: 32-bit feature-major keys, and per pair four arrays of >= n_features * area entries
-        b->sel_stride = 4 * (((int64_t)max_features * area + 63) / 64 * 64);
-        ALLOC(b->d_keys32, ((size_t)n_pairs * b->key_stride + 64) * sizeof(uint32_t));  // +64: K2R reads 16 B at a time
+        // K2R: K1's exact residuals in the reference's feature-major slot order, and the selection scratch
+        b->sel_stride = svo::ref_sel_stride((int64_t)max_features * area);
+        ALLOC(b->d_scratch, (size_t)n_pairs * b->key_stride * sizeof(double));
         ALLOC(b->d_sel, (size_t)n_pairs * b->sel_stride * sizeof(uint32_t));
     } else {
         ALLOC(b->d_scratch, (size_t)n_pairs * b->key_stride * sizeof(double));
@@ -624,7 +623,6 @@ static svo::AlignArgs sub_batch(const svo::AlignArgs& a, const svo_align_batch* 
     s.partials += (int64_t)p0 * b->chunks * 28; s.arrive += p0;
     if (s.keys) s.keys += (int64_t)p0 * b->key_stride;
     if (s.scratch) s.scratch += (int64_t)p0 * b->key_stride;
-    if (s.keys32) s.keys32 += (int64_t)p0 * b->key_stride;
     if (s.sel) s.sel += (int64_t)p0 * b->sel_stride;
     if (s.win) s.win += (int64_t)p0 * b->win_stride;
     s.pose_out += 7 * (int64_t)p0; s.err_out += p0; s.status_out += p0;
@@ -643,7 +641,7 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
     a.xw = b->d_xw; a.keys = b->d_keys; a.key_stride = b->key_stride; a.state = b->d_state; a.partials = b->d_partials;
-    a.keys32 = b->d_keys32; a.sel = b->d_sel; a.sel_stride = b->sel_stride; a.median_mode = b->params.median_mode;
+    a.sel = b->d_sel; a.sel_stride = b->sel_stride; a.median_mode = b->params.median_mode;
     a.arrive = b->d_arrive;
     a.win = b->d_win; a.win_stride = b->win_stride; a.win_levels = b->win_levels;
     a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.cproj = b->d_cproj; a.scratch = b->d_scratch;
@@ -733,24 +731,23 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
         return fail(SVO_ERR_ARG, "need 1 <= n_valid <= n_slots <= 524288 (got %lld, %lld)", (long long)n_valid,
                     (long long)n_slots);
     for (int64_t i = 0; i < n_slots; ++i)
-        if (!(values[i] >= -255.0 && values[i] <= 255.0) && values[i] != 1.7976931348623157e308)
-            return fail(SVO_ERR_ARG, "value %lld = %g outside [-255, 255] and not DBL_MAX", (long long)i, values[i]);
+        if (std::isnan(values[i])) return fail(SVO_ERR_ARG, "value %lld is NaN", (long long)i);
     SVO_HIP(hipSetDevice(c->device));
+    const int64_t sel_stride = svo::ref_sel_stride(n_slots);  // u32
     const int64_t q = (n_slots + 63) / 64 * 64;
-    const size_t bytes = (size_t)q * 8 + (size_t)5 * q * 4 + 2048;
+    const size_t bytes = (size_t)q * 8 + (size_t)sel_stride * 4 + 2048;
     void* base = nullptr;
     hipError_t e = ctx_scratch(c, bytes, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_debug_robust_scale: %s", hipGetErrorString(e));
     SVO_HIP(ctx_ring_drain(c));
     double* d_v = static_cast<double*>(base);
     uint32_t* d_sel = reinterpret_cast<uint32_t*>(d_v + q);
-    double* d_out = reinterpret_cast<double*>(d_sel + 5 * q);  // after the K2R scratch and the keys
+    double* d_out = reinterpret_cast<double*>(d_sel + sel_stride);
     SVO_HIP(hipMemcpyAsync(d_v, values, (size_t)n_slots * 8, hipMemcpyHostToDevice, c->stream));
-    const char* st = getenv("SVO_DEBUG_STAMPS");  // "2": phase stamps of round 1 only (tools/k2r_probe.py)
-    svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, 4 * q, d_out,
-                                   st && st[0] == '2' ? 1 : 0, c->stream);
+    svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, sel_stride, d_out, c->stream);
     SVO_HIP(hipGetLastError());
-    SVO_HIP(hipMemcpyAsync(med_mad, d_out, getenv("SVO_DEBUG_STAMPS") ? 218 * 8 : 16, hipMemcpyDeviceToHost, c->stream));
+    // SVO_DEBUG_STAMPS: also the diagnostics (tools/k2r_probe.py): cycles per pass, round counts, block rounds
+    SVO_HIP(hipMemcpyAsync(med_mad, d_out, getenv("SVO_DEBUG_STAMPS") ? 206 * 8 : 16, hipMemcpyDeviceToHost, c->stream));
     SVO_HIP(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }

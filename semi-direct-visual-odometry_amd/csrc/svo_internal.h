@@ -50,11 +50,11 @@ struct AlignArgs {
     // and pixel).  Slots of features >= n_features are invisible.  Only the 16-bit keys are stored; exact
     // residuals are recomputed from the images where needed (K2 candidates, K3).
     double* cproj;            // scratch [n_pairs*max_f][2] projection (cu, cv) into the cur level (K1)
-    double* scratch;          // scratch [n_pairs][key_stride] exact residuals, written only by K2's exact paths
+    double* scratch;          // scratch [n_pairs][key_stride] exact residuals: K2's exact paths (median_mode 0);
+                              // median_mode 1: K1's residuals in the reference's feature-major slot order
     uint16_t* keys;           // scratch [n_pairs][key_stride] 16-bit monotone key per slot (0xFFFF = invisible)
-    uint32_t* keys32;         // median_mode 1: [n_pairs][key_stride] 32-bit keys (res_key32), feature-major slots
-    uint32_t* sel;            // median_mode 1: [n_pairs][sel_stride] K2R scratch (segment keys, ids, swap partners)
-    int64_t sel_stride;       // u32 per pair: 4 arrays of sel_stride / 4 >= n_features * area entries
+    uint32_t* sel;            // median_mode 1: [n_pairs][sel_stride] K2R scratch (segment, mailbox, step records)
+    int64_t sel_stride;       // u32 per pair: ref_sel_stride(max_f * area)
     int32_t median_mode;      // 0 exact order statistics (K2), 1 the reference's nth_element post-state (K2R)
     int64_t key_stride;       // >= area * round_up(max_f, 64), multiple of 64
     uint32_t* win;            // scratch [n_pairs][win_stride] feature windows of the window levels (K1 -> K3)
@@ -76,7 +76,8 @@ struct AlignArgs {
 void launch_align(const AlignArgs& a, hipStream_t s, hipEvent_t* marks = nullptr);  // marks: see align.hip
 void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s);                 // K2R (align_ref.hip)
 void launch_debug_robust_scale(const double* v, uint32_t M, uint32_t n, uint32_t* sel, int64_t sel_stride, double* out,
-                               int flags, hipStream_t s);
+                               hipStream_t s);
+int64_t ref_sel_stride(int64_t max_slots);  // K2R scratch per pair (u32) for vectors of up to max_slots
 int align_max_half();  // largest patch half size the alignment kernels are instantiated for
 int align_feat_iters();                                 // feature groups per K1/K3 wave
 int align_win_dwords(int half);                         // window dwords per feature (win_stride / slots)
