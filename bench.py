@@ -153,10 +153,14 @@ def main():
         cnt = min(D, P - first)
         ps.upload(3 * first, base[:3 * cnt])
     ctx.synchronize()
-    ctx.record(2)
-    ps.build()
-    ctx.record(3)
-    pyr_ms = ctx.elapsed_ms(2, 3)
+    ps.build()  # warm-up (the first launch loads the code objects)
+    pyr_runs = []
+    for _ in range(5):  # median of 5 builds of all 3P frames (the build is idempotent: level 0 stays)
+        ctx.record(2)
+        ps.build()
+        ctx.record(3)
+        pyr_runs.append(ctx.elapsed_ms(2, 3))
+    pyr_ms = float(np.median(pyr_runs))
     pyr_bytes = 2 * cam["width"] * cam["height"] + 2 * (level_bytes(cam["width"], cam["height"], L)
                                                        - cam["width"] * cam["height"])
 
@@ -282,7 +286,7 @@ def main():
                                "flop_per_pair": 1900 * nf * L,
                                "note": "algorithmic flops (SURVEY 8(d) estimate); the issued VALU instructions are "
                                        "several times more (address, conversion, select): DESIGN 7 SQ counters"},
-        "pyramid_build": {"frames": 3 * P, "ms": round(pyr_ms, 4),
+        "pyramid_build": {"frames": 3 * P, "ms": round(pyr_ms, 4), "statistic": "median of 5 after a warm-up build",
                           "frames_per_s": round(3 * P / (pyr_ms * 1e-3), 1),
                           # algorithmic bytes per frame: read the base image once, write the gradient
                           # base and levels 1.. of both stacks (SURVEY 8(d) pyramid row)
