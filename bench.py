@@ -57,6 +57,9 @@ def parse():
                          "(median_mode SVO_MEDIAN_REFERENCE, K2R); exact = true order statistics (K2)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the config 3 / config 5 lines")
+    ap.add_argument("--core-only", action="store_true",
+                    help="only the timed chain steps (no end-to-end, other-mode or latency runs): PMC passes, whose "
+                         "per-launch bytes assume every align dispatch belongs to the P-pair chain")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: each rank's step is the CPU oracle on its pairs (exercises the multi-rank path)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -231,19 +234,25 @@ def main():
     e2d_s = float(np.median(e2d_runs))
     # the other median semantics on the same pairs: its rate and how far its poses are from the reference's
     other = svo_amd.MEDIAN_EXACT if mode == svo_amd.MEDIAN_REFERENCE else svo_amd.MEDIAN_REFERENCE
-    b2 = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx, median_mode=other)
-    b2.set_pairs(0, ps, ps, ps, *packed)
-    b2.run()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
+    other_line, lat = None, None
+    if not args.core_only:
+        b2 = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx, median_mode=other)
+        b2.set_pairs(0, ps, ps, ps, *packed)
         b2.run()
-    ctx.synchronize()
-    other_s = (time.perf_counter() - t0) / args.steps
-    p2, _, _ = b2.results()
-    b2.close()
-    dpose = max(float(np.abs(canon(p2[i]) - canon(poses[i])).max()) for i in range(D))
-    lat = latency_lines(ctx, scenes, camera, cam, patch, L, nf, mode)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            b2.run()
+        ctx.synchronize()
+        other_s = (time.perf_counter() - t0) / args.steps
+        p2, _, _ = b2.results()
+        b2.close()
+        dpose = max(float(np.abs(canon(p2[i]) - canon(poses[i])).max()) for i in range(D))
+        other_line = {"mode": "exact" if other == svo_amd.MEDIAN_EXACT else "reference",
+                      "pairs_per_s": round(P / other_s, 1), "ms_per_step": round(other_s * 1e3, 4),
+                      "max_abs_pose_param_diff_vs_headline": dpose,
+                      "note": "same pairs; exact order statistics are not the reference's numbers (DESIGN.md)"}
+        lat = latency_lines(ctx, scenes, camera, cam, patch, L, nf, mode)
     if rank != 0:
         if dist:
             dist.barrier()
@@ -298,10 +307,7 @@ def main():
                              if mode == svo_amd.MEDIAN_REFERENCE else "exact order statistics (SVO_MEDIAN_EXACT)"),
         "poses_repeat_bitexact": poses_repeat,
         "step_ms_median_of_20": round(step_med * 1e3, 4),
-        "other_median_mode": {"mode": "exact" if other == svo_amd.MEDIAN_EXACT else "reference",
-                              "pairs_per_s": round(P / other_s, 1), "ms_per_step": round(other_s * 1e3, 4),
-                              "max_abs_pose_param_diff_vs_headline": dpose,
-                              "note": "same pairs; exact order statistics are not the reference's numbers (DESIGN.md)"},
+        "other_median_mode": other_line,
         "end_to_end": {"pairs": P, "ms": round(e2e_s * 1e3, 3), "pairs_per_s": round(P / e2e_s, 1),
                        "note": "from host memory: H2D of 3P base images (pageable), pyramid build, all pairs' "
                                "features / poses in one svo_align_batch_set_pairs call, alignment, D2H of the results"},

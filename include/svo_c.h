@@ -176,9 +176,10 @@ int svo_align_batch_traces(svo_align_batch* batch, int32_t pair, svo_level_trace
 
 /* Diagnostics (no reference counterpart): the SVO_MEDIAN_REFERENCE robust scale of an arbitrary residual
  * vector, i.e. algorithm::computeMAD(values, n_valid) (src/algorithm.cpp:855-865) and the median it uses, on
- * the device.  values: n_slots entries in [-255, 255] or DBL_MAX (an invisible slot); med_mad[0] = median,
+ * the device.  values: n_slots doubles, none NaN (an invisible slot is DBL_MAX); med_mad[0] = median,
  * med_mad[1] = MAD.  Synchronous.  With the environment variable SVO_DEBUG_STAMPS set, med_mad must hold
- * 218 doubles: [2..31] cycle stamps per phase, [32..217] per-round logs (tools/k2r_probe.py). */
+ * 206 doubles: [2..9] cycles / block rounds / one-wave rounds / heap select per pass, [10..189] the block
+ * rounds (segment size, where it lived, cycles), [190..205] cycles per round phase (tools/k2r_probe.py). */
 int svo_debug_robust_scale(svo_ctx* ctx, const double* values, int64_t n_slots, int64_t n_valid, double* med_mad);
 
 /* ---------------------------------------------------------------- FeatureAlignment

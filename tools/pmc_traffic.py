@@ -26,7 +26,7 @@ def per_kernel(pass_dir, counter):
             if "svo::align" not in name or r["Counter_Name"] != counter:
                 continue
             tot[name.split("(")[0]] += float(r["Counter_Value"]) * 1024.0
-            if "align_scale_kernel" in name:
+            if "align_scale_kernel" in name or "align_scale_ref_kernel" in name:  # K2 / K2R: once per level and chain
                 runs += 1
     return tot, runs
 
@@ -53,6 +53,8 @@ def main():
         "hbm_bytes_per_launch": round(total), "hbm_bytes_per_pair": round(total / a.pairs),
         "per_kernel_bytes_per_launch": {k: {kk: round(vv) for kk, vv in v.items()} for k, v in per.items()},
         "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes",
+        "calibration_note": "MI355X_MICROARCH.md calibrates the FETCH_SIZE x2 only for 16-B/lane coalesced streams; "
+                            "the 8-B/lane gathers of K1/K2R are uncalibrated, so the read bytes are an estimate",
     }, indent=1))
 
 
