@@ -127,3 +127,31 @@ def test_align_reference_mode_matches_oracle(cfg):
         assert np.abs(canon(poses[i]) - canon(pose_c)).max() <= 1e-9
         assert abs(err[i] - err_c) <= 1e-9 * abs(err_c)
         assert st[i] == st_c
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_slots", [98000, 300000])
+def test_debug_robust_scale_large_vectors(n_slots):
+    """Vectors past 64512 slots take K2R's large instantiation (step records in the pair's global scratch,
+    17 register rows of block prefixes): patch 7 at 2000 features is 98000 slots."""
+    rng = np.random.default_rng(n_slots)
+    v = rng.normal(0, 8, n_slots)
+    v[rng.random(n_slots) < 0.15] = DBL_MAX
+    n = int((v < DBL_MAX).sum())
+    med, mad = svo_amd.debug_robust_scale(v, n)
+    med_c, mad_c = oracle_med_mad(v, n)
+    assert med == med_c and mad == mad_c, (med, med_c, mad, mad_c)
+
+
+@pytest.mark.gpu
+def test_align_reference_mode_large_vector():
+    """A whole alignment whose residual vector exceeds 64512 slots (patch 7, 2000 features: 98000)."""
+    pairs = make_pairs(2, n_features=2000, patch_size=7)
+    b, _ = gpu_batch(pairs, 7, 1, 3, median_mode=svo_amd.MEDIAN_REFERENCE)
+    b.run()
+    poses, err, st = b.results()
+    for i, s in enumerate(pairs):
+        pose_c, err_c, st_c, tr_c = oracle_align(s, 7, 1, 3, mode=0)
+        _check_ref_traces(b.traces(i), tr_c, 1, 3)
+        assert np.abs(canon(poses[i]) - canon(pose_c)).max() <= 1e-9
+        assert st[i] == st_c
