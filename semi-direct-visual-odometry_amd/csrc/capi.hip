@@ -61,6 +61,7 @@ struct svo_ctx {
     hipStream_t stream;
     hipStream_t sides[4];         // extra streams: a batch runs as concurrent sub-batch chains
     hipEvent_t fork, joins[4];    // sides wait for stream at fork; stream waits for each side at its join
+    hipEvent_t chain_marks[2 + 3 * svo::kMaxLevels];  // launch marks of chain 0 (the staggered start of chain 1)
     hipEvent_t events[16];
     // grow-only scratch of the synchronous per-call entry points (FeatureAlignment): no device
     // allocation per call once warm
@@ -197,6 +198,8 @@ int svo_ctx_create(int32_t device, svo_ctx** out) {
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->sides[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->joins[i], hipEventDisableTiming);
+    for (int i = 0; i < 2 + 3 * svo::kMaxLevels && e == hipSuccess; ++i)
+        e = hipEventCreateWithFlags(&c->chain_marks[i], hipEventDisableTiming);
     for (int i = 0; i < 16 && e == hipSuccess; ++i) e = hipEventCreate(&c->events[i]);
     if (e != hipSuccess) {
         delete c;
@@ -213,6 +216,8 @@ int svo_ctx_destroy(svo_ctx* c) {
     for (hipEvent_t ev : c->events)
         if (ev) (void)hipEventDestroy(ev);
     if (c->fork) (void)hipEventDestroy(c->fork);
+    for (hipEvent_t ev : c->chain_marks)
+        if (ev) (void)hipEventDestroy(ev);
     for (int i = 1; i < 4; ++i) {
         if (c->joins[i]) (void)hipEventDestroy(c->joins[i]);
         if (c->sides[i]) (void)hipStreamDestroy(c->sides[i]);
@@ -659,11 +664,16 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         // independent of the split.
         const int ns = kSplits;
         const int32_t per = (b->n_pairs / ns + 7) / 8 * 8;
+        // SVO_STAGGER=k (measurement): chain 1 starts after chain 0's k-th launch mark (1 + 3 per level)
+        const char* sg = getenv("SVO_STAGGER");
+        const int stagger = sg ? atoi(sg) : 0;
         SVO_HIP(hipEventRecord(c->fork, c->stream));
         for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->fork, 0));
         for (int i = 0; i < ns; ++i) {
             const int32_t p0 = i * per, cnt = i == ns - 1 ? b->n_pairs - p0 : per;
-            svo::launch_align(sub_batch(a, b, p0, cnt), i == 0 ? c->stream : c->sides[i], nullptr);
+            if (i == 1 && stagger > 0) SVO_HIP(hipStreamWaitEvent(c->sides[1], c->chain_marks[stagger], 0));
+            svo::launch_align(sub_batch(a, b, p0, cnt), i == 0 ? c->stream : c->sides[i],
+                              i == 0 && stagger > 0 ? c->chain_marks : nullptr);
         }
         for (int i = 1; i < ns; ++i) {
             SVO_HIP(hipEventRecord(c->joins[i], c->sides[i]));
