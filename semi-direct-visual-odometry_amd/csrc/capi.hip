@@ -664,9 +664,14 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         // independent of the split.
         const int ns = kSplits;
         const int32_t per = (b->n_pairs / ns + 7) / 8 * 8;
-        // SVO_STAGGER=k (measurement): chain 1 starts after chain 0's k-th launch mark (1 + 3 per level)
+        // Reference semantics: chain 1 starts when chain 0's first K1 is done (launch mark 2), so that each
+        // chain's K1 / K3 run under the other chain's K2R instead of both chains meeting in K1 / K3 at every
+        // level (MI355X, 512 pairs: 88.4k vs 78.4k pairs/s; marks 3 / 4 / 7: 79k / 74k / 67k).  The exact mode
+        // runs unstaggered (round 1: staggering by 1-3 kernels cost 1-6 %).  SVO_STAGGER=k overrides.
         const char* sg = getenv("SVO_STAGGER");
-        const int stagger = sg ? atoi(sg) : 0;
+        const int stagger = sg ? atoi(sg) : (b->params.median_mode == SVO_MEDIAN_REFERENCE ? 2 : 0);
+        if (stagger < 0 || stagger > 1 + 3 * (b->params.max_level - b->params.min_level + 1))
+            return fail(SVO_ERR_ARG, "SVO_STAGGER=%d outside the chain's launch marks", stagger);
         SVO_HIP(hipEventRecord(c->fork, c->stream));
         for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->fork, 0));
         for (int i = 0; i < ns; ++i) {
