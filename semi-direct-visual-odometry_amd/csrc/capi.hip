@@ -61,7 +61,7 @@ struct svo_ctx {
     hipStream_t stream;
     hipStream_t sides[4];         // extra streams: a batch runs as concurrent sub-batch chains
     hipEvent_t fork, joins[4];    // sides wait for stream at fork; stream waits for each side at its join
-    hipEvent_t chain_marks[2 + 3 * svo::kMaxLevels];  // launch marks of chain 0 (the staggered start of chain 1)
+    hipEvent_t chain_marks[3][2 + 3 * svo::kMaxLevels];  // launch marks of chains 0..2 (staggered starts)
     hipEvent_t events[16];
     // grow-only scratch of the synchronous per-call entry points (FeatureAlignment): no device
     // allocation per call once warm
@@ -198,8 +198,9 @@ int svo_ctx_create(int32_t device, svo_ctx** out) {
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->sides[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->joins[i], hipEventDisableTiming);
-    for (int i = 0; i < 2 + 3 * svo::kMaxLevels && e == hipSuccess; ++i)
-        e = hipEventCreateWithFlags(&c->chain_marks[i], hipEventDisableTiming);
+    for (int k = 0; k < 3; ++k)
+        for (int i = 0; i < 2 + 3 * svo::kMaxLevels && e == hipSuccess; ++i)
+            e = hipEventCreateWithFlags(&c->chain_marks[k][i], hipEventDisableTiming);
     for (int i = 0; i < 16 && e == hipSuccess; ++i) e = hipEventCreate(&c->events[i]);
     if (e != hipSuccess) {
         delete c;
@@ -216,8 +217,9 @@ int svo_ctx_destroy(svo_ctx* c) {
     for (hipEvent_t ev : c->events)
         if (ev) (void)hipEventDestroy(ev);
     if (c->fork) (void)hipEventDestroy(c->fork);
-    for (hipEvent_t ev : c->chain_marks)
-        if (ev) (void)hipEventDestroy(ev);
+    for (auto& row : c->chain_marks)
+        for (hipEvent_t ev : row)
+            if (ev) (void)hipEventDestroy(ev);
     for (int i = 1; i < 4; ++i) {
         if (c->joins[i]) (void)hipEventDestroy(c->joins[i]);
         if (c->sides[i]) (void)hipStreamDestroy(c->sides[i]);
@@ -662,7 +664,8 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         // two independent half-batch chains on two streams: one chain's latency-bound stages (the
         // per-pair robust scale) overlap the other chain's feature stages.  Results are per pair and
         // independent of the split.
-        const int ns = kSplits;
+        const char* sc = getenv("SVO_CHAINS");  // (measurement: 2..4 concurrent chains)
+        const int ns = sc ? std::max(2, std::min(4, atoi(sc))) : kSplits;
         const int32_t per = (b->n_pairs / ns + 7) / 8 * 8;
         // Reference semantics: chain 1 starts when chain 0's first K1 is done (launch mark 2), so that each
         // chain's K1 / K3 run under the other chain's K2R instead of both chains meeting in K1 / K3 at every
@@ -676,9 +679,10 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->fork, 0));
         for (int i = 0; i < ns; ++i) {
             const int32_t p0 = i * per, cnt = i == ns - 1 ? b->n_pairs - p0 : per;
-            if (i == 1 && stagger > 0) SVO_HIP(hipStreamWaitEvent(c->sides[1], c->chain_marks[stagger], 0));
+            if (cnt <= 0) continue;
+            if (i >= 1 && stagger > 0) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->chain_marks[i - 1][stagger], 0));
             svo::launch_align(sub_batch(a, b, p0, cnt), i == 0 ? c->stream : c->sides[i],
-                              i == 0 && stagger > 0 ? c->chain_marks : nullptr);
+                              i < ns - 1 && stagger > 0 ? c->chain_marks[i] : nullptr);
         }
         for (int i = 1; i < ns; ++i) {
             SVO_HIP(hipEventRecord(c->joins[i], c->sides[i]));
