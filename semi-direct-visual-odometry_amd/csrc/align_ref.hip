@@ -593,6 +593,8 @@ struct RefSel {
             uint64_t ge[8], le[8];
             uint32_t gp[8], lp[8];  // #GE / #LE before each step
             uint32_t tG = 0, tL = 0;
+            // only the steps the segment touches do vector work (the later rounds span one or two)
+            const uint32_t js = fr / 64u, je = (lr + 63u) / 64u;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const uint32_t i = 64u * (uint32_t)j + me;
@@ -641,6 +643,7 @@ struct RefSel {
             // sources to the mailbox, then the kept side's targets read it
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
+                if ((uint32_t)j < js || (uint32_t)j >= je) continue;
                 uint32_t k = kNone;
                 if (right) {
                     const uint32_t kk = gp[j] + lanes_below(ge[j]) + 1u;
@@ -653,6 +656,7 @@ struct RefSel {
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
+                if ((uint32_t)j < js || (uint32_t)j >= je) continue;
                 uint32_t k = kNone;
                 if (right) {
                     const uint32_t kk = tL - (lp[j] + lanes_below(le[j]));
