@@ -113,15 +113,19 @@ __global__ void __launch_bounds__(kGradThreads) abs_grad_kernel(uint8_t* stacks,
         *reinterpret_cast<uint4*>(st + o) = *reinterpret_cast<const uint4*>(src + s0 + o);
     for (int64_t o = full + threadIdx.x; o < s1 - s0; o += kGradThreads) st[o] = src[s0 + o];
     __syncthreads();
-    const int64_t q0 = p0 + (int64_t)threadIdx.x * 16;
-    if (q0 >= npx) return;
-    const int y = (int)(q0 / w), x = (int)(q0 - (int64_t)y * w);
-    const int n = npx - q0 < 16 ? (int)(npx - q0) : 16;
-    const int yl = (int)((q0 + n - 1) / w);
-    const int c0 = (int)(q0 - s0);  // 16-B aligned LDS offset of the run
+    // 32-bit index math (planes are < 2^31 px; 64-bit divisions were a large part of the kernel)
+    const uint32_t q0 = (uint32_t)p0 + (uint32_t)threadIdx.x * 16u, NPX = (uint32_t)npx, W = (uint32_t)w;
+    if (q0 >= NPX) return;
+    const uint32_t y = q0 / W, x = q0 - y * W;
+    const int n = NPX - q0 < 16u ? (int)(NPX - q0) : 16;
+    const int c0 = (int)(q0 - (uint32_t)s0);  // 16-B aligned LDS offset of the run
     uint32_t out[4];
-    if (n == 16 && y > 0 && yl < h - 1 && x > 0 && x + 15 < w - 1) {
-        // interior run of one row: aligned dword LDS reads realigned with v_alignbyte
+    if (n == 16 && w >= 32 && c0 >= w) {  // (c0 < w: the plane's first row; up-neighbours unstaged)
+        // every full group on the byte-parallel path (aligned dword LDS reads realigned with v_alignbyte),
+        // including groups that wrap onto the next row (the flat layout keeps every non-border pixel's four
+        // neighbours right); pixels on the image border (Simd leaves them 0) are cleared afterwards.
+        // Reads past the staged bytes (the last row's down-neighbours) stay inside the array and only feed
+        // cleared pixels.
         const uint32_t* sd = reinterpret_cast<const uint32_t*>(st);
         uint32_t C[6], U[5], D[5];
 #pragma unroll
@@ -137,8 +141,24 @@ __global__ void __launch_bounds__(kGradThreads) abs_grad_kernel(uint8_t* stacks,
         for (int i = 0; i < 4; ++i)
             out[i] = grad4(__builtin_amdgcn_alignbyte(C[i + 1], C[i], 3), __builtin_amdgcn_alignbyte(C[i + 2], C[i + 1], 1),
                            __builtin_amdgcn_alignbyte(U[i + 1], U[i], su), __builtin_amdgcn_alignbyte(D[i + 1], D[i], sdn));
+        // border pixels of the group: bit i for pixel q0 + i (w >= 32: at most one row end inside)
+        const uint32_t rem = W - x;  // pixels of row y from q0 on
+        const uint32_t in_y = rem >= 16u ? 0xFFFFu : (1u << rem) - 1u;
+        uint32_t z = 0;
+        if (y == 0 || y == (uint32_t)h - 1) z |= in_y;
+        if (rem < 16u && y + 1 == (uint32_t)h - 1) z |= 0xFFFFu & ~in_y;
+        if (x == 0) z |= 1u;
+        if (rem <= 16u) z |= 1u << (rem - 1);  // column w - 1
+        if (rem < 16u) z |= 1u << rem;         // column 0 of row y + 1
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t zb = (z >> (4 * i)) & 0xFu;
+            const uint32_t m = ((zb & 1u) ? 0xFFu : 0u) | ((zb & 2u) ? 0xFF00u : 0u) | ((zb & 4u) ? 0xFF0000u : 0u) |
+                               ((zb & 8u) ? 0xFF000000u : 0u);
+            out[i] &= ~m;
+        }
     } else {
-        int yy = y, xx = x;
+        int yy = (int)y, xx = (int)x;
         out[0] = out[1] = out[2] = out[3] = 0;
         for (int i = 0; i < n; ++i) {
             uint32_t g = 0;
