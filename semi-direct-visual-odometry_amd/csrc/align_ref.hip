@@ -30,6 +30,8 @@
 // the depth limit falls back to the restated heap select (one lane; adversarial inputs only), the last
 // <= 3 values are sorted.  vec[n/2 - 1] is recorded at the round whose cut lands exactly on n/2 (that slot is
 // never touched again), or read after the final sort.
+#include <cstdlib>
+
 #include "svo_internal.h"
 #include "svo_math.h"
 #include "svo_wave.h"
@@ -38,10 +40,14 @@ namespace svo {
 
 namespace {
 
-constexpr int kRT = 512;                     // threads per pair
-constexpr int kRW = kRT / 64;                // waves
-constexpr uint32_t kBlk = 512;               // positions per block (8 steps of 64), owned by wave block % kRW
-constexpr uint32_t kCap = 9 * kBlk;          // LDS segment capacity: positions from a block-aligned base
+constexpr uint32_t kBlk = 512;               // positions per block (8 steps of 64), owned by wave block % TW
+// TW waves per pair: 8 (512 threads, two pairs per CU: batches of more than 128 pairs per launch) or 16
+// (1024 threads, one pair per CU with a 20-block LDS segment: small batches, the per-frame latency)
+template <int TW>
+struct Geo {
+    static constexpr int RT = 64 * TW;
+    static constexpr uint32_t Cap = (TW == 8 ? 9u : 20u) * kBlk;  // LDS segment capacity (block-aligned base)
+};
 constexpr uint32_t kRecSteps = 1024;         // LDS step records (absolute steps): vectors of <= 64512 slots
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr double kDblMax = 1.7976931348623157e308;
@@ -49,9 +55,10 @@ constexpr int kLogCap = 60;                  // diagnostics: block rounds logged
 
 enum { kSrc = 0, kGlb = 1, kLds = 2 };  // where the current segment lives
 
-template <int NB>
+template <int NB, int TW>
 struct RefShared {
     static constexpr uint32_t kRec = NB <= 2 ? kRecSteps : 1;  // (NB > 2: the records are global)
+    static constexpr uint32_t kCap = Geo<TW>::Cap;
     double seg[kCap];               // the segment, from position `base`
     double mb[kCap / 2];            // mailbox of LDS rounds (Ks <= S / 2) and of the one-wave rounds
     uint64_t msk[kRec][2];          // per step: GE, LE ballots
@@ -168,10 +175,12 @@ __device__ __attribute__((noinline)) void heap_select_fn(double* seg, uint32_t b
 
 // NB: rows of 64 blocks held in registers by the block scans (2: M <= 64512, 17: M <= 524288).  With NB = 2
 // the step records live in LDS (absolute steps), else in the pair's global scratch.
-template <int NB, bool kSt>
+template <int NB, int TW, bool kSt>
 struct RefSel {
     static constexpr bool kRecLds = NB <= 2;
-    using Sh = RefShared<NB>;
+    static constexpr int kRW = TW, kRT = Geo<TW>::RT;
+    static constexpr uint32_t kCap = Geo<TW>::Cap;
+    using Sh = RefShared<NB, TW>;
     Sh& sh;
     Diag* dg;
     const double* src;  // the pass's source vector (K1's residuals, reference slot order), read-only
@@ -759,12 +768,12 @@ struct RefSel {
 
 // computeMedian / computeMAD (src/algorithm.cpp:834-865) with the reference's post-state: thread 0 of the
 // block gets med and mad.  M slots, n visible; sel: the pair's scratch (sel_stride u32).
-template <int NB, bool kSt>
-__device__ __forceinline__ void ref_robust_scale(const double* src, RefShared<NB>& sh, Diag* dg, uint32_t* sel,
+template <int NB, int TW, bool kSt>
+__device__ __forceinline__ void ref_robust_scale(const double* src, RefShared<NB, TW>& sh, Diag* dg, uint32_t* sel,
                                                  int64_t sel_stride, uint32_t M, uint32_t n, double& med, double& mad) {
     const int tid = (int)threadIdx.x;
     const int64_t mp = sel_stride / 4;  // positions the scratch holds (a multiple of kBlk, >= M + kBlk)
-    RefSel<NB, kSt> s{sh, dg};
+    RefSel<NB, TW, kSt> s{sh, dg};
     s.src = src;
     s.gseg = reinterpret_cast<double*>(sel);
     s.gmb = s.gseg + mp;
@@ -790,8 +799,9 @@ __device__ __forceinline__ void ref_robust_scale(const double* src, RefShared<NB
     }
 }
 
-template <int NB>
-__device__ __forceinline__ void scale_ref_pair(const AlignArgs& a, int level, RefShared<NB>& sh) {
+template <int NB, int TW>
+__device__ __forceinline__ void scale_ref_pair(const AlignArgs& a, int level, RefShared<NB, TW>& sh) {
+    constexpr int kRT = Geo<TW>::RT, kRW = TW;
     const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     PairState& S = a.state[pair];
     if (!S.active) return;
@@ -815,7 +825,7 @@ __device__ __forceinline__ void scale_ref_pair(const AlignArgs& a, int level, Re
     const uint32_t n = ncv * (uint32_t)a.area;
     double med = kDblMax, mad = 0.0;  // n == 0: every slot is DBL_MAX in the reference
     if (n > 0)
-        ref_robust_scale<NB, false>(a.scratch + (int64_t)pair * a.key_stride, sh, nullptr,
+        ref_robust_scale<NB, TW, false>(a.scratch + (int64_t)pair * a.key_stride, sh, nullptr,
                                     a.sel + (int64_t)pair * a.sel_stride, a.sel_stride, M, n, med, mad);
     if (tid == 0) {
         double sigma = 1.482602218505602 * mad;
@@ -834,17 +844,18 @@ constexpr uint32_t kSmallM = 64u * 2u * kBlk - 2u * kBlk;  // NB = 2 covers ever
 }  // namespace
 
 // K2R: one workgroup per pair, two per CU (replaces align_scale_kernel when median_mode = SVO_MEDIAN_REFERENCE).
-template <int NB>
-__global__ void __launch_bounds__(kRT, 2) __attribute__((amdgpu_waves_per_eu(4, 4))) align_scale_ref_kernel(AlignArgs a, int level) {
-    __shared__ RefShared<NB> sh;
-    scale_ref_pair<NB>(a, level, sh);
+template <int NB, int TW>
+__global__ void __launch_bounds__(Geo<TW>::RT, TW == 8 ? 2 : 1) __attribute__((amdgpu_waves_per_eu(4, 4)))
+align_scale_ref_kernel(AlignArgs a, int level) {
+    __shared__ RefShared<NB, TW> sh;
+    scale_ref_pair<NB, TW>(a, level, sh);
 }
 
 // svo_debug_robust_scale: the same selection on an arbitrary residual vector (one workgroup)
-template <int NB>
-__global__ void __launch_bounds__(kRT, 2) debug_robust_scale_kernel(const double* v, uint32_t M, uint32_t n, uint32_t* sel,
+template <int NB, int TW>
+__global__ void __launch_bounds__(Geo<TW>::RT, TW == 8 ? 2 : 1) debug_robust_scale_kernel(const double* v, uint32_t M, uint32_t n, uint32_t* sel,
                                                                    int64_t sel_stride, double* out) {
-    __shared__ RefShared<NB> sh;
+    __shared__ RefShared<NB, TW> sh;
     __shared__ Diag dg;
     if (threadIdx.x == 0) {
         dg.cyc[0] = dg.cyc[1] = 0;
@@ -854,7 +865,7 @@ __global__ void __launch_bounds__(kRT, 2) debug_robust_scale_kernel(const double
     }
     __syncthreads();
     double med = 0.0, mad = 0.0;
-    ref_robust_scale<NB, true>(v, sh, &dg, sel, sel_stride, M, n, med, mad);
+    ref_robust_scale<NB, TW, true>(v, sh, &dg, sel, sel_stride, M, n, med, mad);
     if (threadIdx.x == 0) {
         out[0] = med;
         out[1] = mad;
@@ -869,24 +880,32 @@ __global__ void __launch_bounds__(kRT, 2) debug_robust_scale_kernel(const double
     }
 }
 
-int ref_threads() { return kRT; }
+int ref_threads() { return Geo<8>::RT; }
 // K2R scratch per pair, in u32: the segment (mp doubles), the mailbox (mp / 2), step records
 int64_t ref_sel_stride(int64_t max_slots) {
     const int64_t mp = (max_slots + kBlk - 1) / kBlk * kBlk + kBlk;
     return 4 * mp;
 }
 void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s) {
-    if ((int64_t)a.max_f * a.area <= (int64_t)kSmallM)
-        hipLaunchKernelGGL(align_scale_ref_kernel<2>, dim3(a.n_pairs), dim3(kRT), 0, s, a, level);
-    else
-        hipLaunchKernelGGL(align_scale_ref_kernel<17>, dim3(a.n_pairs), dim3(kRT), 0, s, a, level);
+    // a launch of at most 128 pairs (small batches, one pair per frame) gives each pair a whole CU
+    const bool wide = a.n_pairs <= 128;
+    const bool small = (int64_t)a.max_f * a.area <= (int64_t)kSmallM;
+    if (small && wide) hipLaunchKernelGGL((align_scale_ref_kernel<2, 16>), dim3(a.n_pairs), dim3(Geo<16>::RT), 0, s, a, level);
+    else if (small) hipLaunchKernelGGL((align_scale_ref_kernel<2, 8>), dim3(a.n_pairs), dim3(Geo<8>::RT), 0, s, a, level);
+    else if (wide) hipLaunchKernelGGL((align_scale_ref_kernel<17, 16>), dim3(a.n_pairs), dim3(Geo<16>::RT), 0, s, a, level);
+    else hipLaunchKernelGGL((align_scale_ref_kernel<17, 8>), dim3(a.n_pairs), dim3(Geo<8>::RT), 0, s, a, level);
 }
 void launch_debug_robust_scale(const double* v, uint32_t M, uint32_t n, uint32_t* sel, int64_t sel_stride, double* out,
                                hipStream_t s) {
-    if (M <= kSmallM)
-        hipLaunchKernelGGL(debug_robust_scale_kernel<2>, dim3(1), dim3(kRT), 0, s, v, M, n, sel, sel_stride, out);
-    else
-        hipLaunchKernelGGL(debug_robust_scale_kernel<17>, dim3(1), dim3(kRT), 0, s, v, M, n, sel, sel_stride, out);
+    // (SVO_K2R_WAVES=16: the 16-wave instantiation, as small batches run it)
+    static const bool w16 = getenv("SVO_K2R_WAVES") && atoi(getenv("SVO_K2R_WAVES")) == 16;
+    if (M <= kSmallM) {
+        if (w16) hipLaunchKernelGGL((debug_robust_scale_kernel<2, 16>), dim3(1), dim3(Geo<16>::RT), 0, s, v, M, n, sel, sel_stride, out);
+        else hipLaunchKernelGGL((debug_robust_scale_kernel<2, 8>), dim3(1), dim3(Geo<8>::RT), 0, s, v, M, n, sel, sel_stride, out);
+    } else {
+        if (w16) hipLaunchKernelGGL((debug_robust_scale_kernel<17, 16>), dim3(1), dim3(Geo<16>::RT), 0, s, v, M, n, sel, sel_stride, out);
+        else hipLaunchKernelGGL((debug_robust_scale_kernel<17, 8>), dim3(1), dim3(Geo<8>::RT), 0, s, v, M, n, sel, sel_stride, out);
+    }
 }
 
 }  // namespace svo
