@@ -97,3 +97,35 @@ def test_gpu_two_chain_batch(mode):
         assert np.array_equal(pb, poses) and np.array_equal(eb, err) and np.array_equal(sb, st)
         bb.close()
     b.close()
+
+
+@pytest.mark.gpu
+def test_gpu_wide_launch_instantiation():
+    """Launches of more than 128 pairs run K2R's 8-wave instantiation (two pairs per CU, the headline's);
+    smaller ones the 16-wave one.  264 pairs = two chains of 136: every pair against the oracle's
+    std::nth_element path and bit for bit against a single-pair (16-wave) run of its scene."""
+    ctx = svo_amd.default_context()
+    sc = scenes()
+    ps = pyramids(sc, ctx)
+    cam = camera_of(sc[0])
+    n = 264
+    b = svo_amd.AlignBatch(cam, PATCH, 0, L - 1, n, NF, ctx, median_mode=svo_amd.MEDIAN_REFERENCE)
+    b.set_pairs(0, ps, ps, ps, *packed(sc, range(n)))
+    b.run()
+    poses, err, st = b.results()
+    ref = [oracle_align(s, PATCH, 0, L - 1, mode=0, trace=False) for s in sc]
+    for i in range(n):
+        pc, ec, stc = ref[i % D][:3]
+        assert st[i] == stc, i
+        assert np.abs(canon(poses[i]) - canon(pc)).max() <= 1e-9, i
+    for d in range(D):
+        s = sc[d]
+        b1 = svo_amd.AlignBatch(cam, PATCH, 0, L - 1, 1, NF, ctx, median_mode=svo_amd.MEDIAN_REFERENCE)
+        b1.set_pair(0, (ps, 3 * d), (ps, 3 * d + 1), (ps, 3 * d + 2), s.ref_pose, s.kf_pose, s.cur_init_pose,
+                    s.n_ref, s.n_kf, s.px, s.bearing, s.point, s.has_point)
+        b1.run()
+        p1, e1, s1 = b1.results()
+        b1.close()
+        for i in (d, d + 132, n - D + d):  # both chains
+            assert np.array_equal(p1[0], poses[i]) and e1[0] == err[i] and s1[0] == st[i], (d, i)
+    b.close()
