@@ -63,6 +63,10 @@ struct svo_ctx {
     hipEvent_t fork, joins[4];    // sides wait for stream at fork; stream waits for each side at its join
     hipEvent_t chain_marks[3][2 + 3 * svo::kMaxLevels];  // launch marks of chains 0..2 (staggered starts)
     hipEvent_t events[16];
+    // svo_align_batch_set_pairs uploads on its own stream, so the copies overlap a pyramid build queued
+    // on `stream`; staged: the upload is done; stage_free: the last scatter out of a staging block is done
+    hipStream_t copy;
+    hipEvent_t staged, stage_free;
     // grow-only scratch of the synchronous per-call entry points (FeatureAlignment): no device
     // allocation per call once warm
     void* scratch = nullptr;
@@ -196,7 +200,10 @@ int svo_ctx_create(int32_t device, svo_ctx** out) {
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->sides[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->stage_free, hipEventDisableTiming);
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&c->joins[i], hipEventDisableTiming);
     for (int k = 0; k < 3; ++k)
         for (int i = 0; i < 2 + 3 * svo::kMaxLevels && e == hipSuccess; ++i)
@@ -216,7 +223,11 @@ int svo_ctx_destroy(svo_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     for (hipEvent_t ev : c->events)
         if (ev) (void)hipEventDestroy(ev);
+    if (c->copy) (void)hipStreamSynchronize(c->copy);
     if (c->fork) (void)hipEventDestroy(c->fork);
+    if (c->staged) (void)hipEventDestroy(c->staged);
+    if (c->stage_free) (void)hipEventDestroy(c->stage_free);
+    if (c->copy) (void)hipStreamDestroy(c->copy);
     for (auto& row : c->chain_marks)
         for (hipEvent_t ev : row)
             if (ev) (void)hipEventDestroy(ev);
@@ -567,45 +578,58 @@ int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, 
         d.n_ref = n_feat[2 * i];
         d.n_kf = n_feat[2 * i + 1];
     }
-    // device staging: the row offsets, then (host features) the packed arrays
+    // device staging: the row offsets, the pair descriptors, then (host features) the packed arrays
     const size_t off_bytes = ((size_t)(count + 1) * sizeof(int64_t) + 255) / 256 * 256;
+    const size_t desc_bytes = (sizeof(svo::PairDesc) * count + 255) / 256 * 256;
     const size_t host_bytes = features_on_device ? 0 : (size_t)T * 65 + 4 * 256;
-    const size_t need = off_bytes + host_bytes;
+    const size_t need = off_bytes + desc_bytes + host_bytes;
     if (need > b->stage_bytes) {
-        if (b->d_stage) SVO_HIP(hipFree(b->d_stage));
+        if (b->d_stage) {  // a scatter queued on the stream may still read the old block
+            SVO_HIP(hipStreamSynchronize(b->ctx->stream));
+            SVO_HIP(hipFree(b->d_stage));
+        }
         b->d_stage = nullptr;
         b->stage_bytes = 0;
         SVO_HIP(hipMalloc(&b->d_stage, need + need / 4));
         b->stage_bytes = need + need / 4;
     }
     svo_ctx* c = b->ctx;
-    hipStream_t s = c->stream;
+    hipStream_t s = c->stream, cs = c->copy;
     SVO_HIP(ctx_ring_drain(c));  // set_pair copies still reading the ring go first (stream order anyway)
+    // the upload runs on the copy stream, behind only the previous scatter out of staging (not behind
+    // whatever else `stream` holds, e.g. the pyramid build these pairs read); `stream` then waits for it
+    SVO_HIP(hipStreamWaitEvent(cs, c->stage_free, 0));
     int64_t* d_off = reinterpret_cast<int64_t*>(b->d_stage);
-    SVO_HIP(hipMemcpyAsync(d_off, off.data(), (size_t)(count + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    SVO_HIP(hipMemcpyAsync(b->d_pairs + first, b->h_pairs.data() + first, sizeof(svo::PairDesc) * count,
-                           hipMemcpyHostToDevice, s));
+    svo::PairDesc* d_desc = reinterpret_cast<svo::PairDesc*>(b->d_stage + off_bytes);
+    SVO_HIP(hipMemcpyAsync(d_off, off.data(), (size_t)(count + 1) * sizeof(int64_t), hipMemcpyHostToDevice, cs));
+    SVO_HIP(hipMemcpyAsync(d_desc, b->h_pairs.data() + first, sizeof(svo::PairDesc) * count, hipMemcpyHostToDevice,
+                           cs));
     const double *spx = px, *sbr = bearing, *spt = point;
     const uint8_t* shp = has_point;
     if (!features_on_device && T > 0) {
         auto r256 = [](size_t v) { return (v + 255) / 256 * 256; };
-        uint8_t* p = b->d_stage + off_bytes;
+        uint8_t* p = b->d_stage + off_bytes + desc_bytes;
         double* dpx = reinterpret_cast<double*>(p);
         double* dbr = reinterpret_cast<double*>(p + r256((size_t)T * 16));
         double* dpt = reinterpret_cast<double*>(p + r256((size_t)T * 16) + r256((size_t)T * 24));
         uint8_t* dhp = p + r256((size_t)T * 16) + 2 * r256((size_t)T * 24);
-        SVO_HIP(hipMemcpyAsync(dpx, px, (size_t)T * 16, hipMemcpyHostToDevice, s));
-        SVO_HIP(hipMemcpyAsync(dbr, bearing, (size_t)T * 24, hipMemcpyHostToDevice, s));
-        SVO_HIP(hipMemcpyAsync(dpt, point, (size_t)T * 24, hipMemcpyHostToDevice, s));
-        SVO_HIP(hipMemcpyAsync(dhp, has_point, (size_t)T, hipMemcpyHostToDevice, s));
+        SVO_HIP(hipMemcpyAsync(dpx, px, (size_t)T * 16, hipMemcpyHostToDevice, cs));
+        SVO_HIP(hipMemcpyAsync(dbr, bearing, (size_t)T * 24, hipMemcpyHostToDevice, cs));
+        SVO_HIP(hipMemcpyAsync(dpt, point, (size_t)T * 24, hipMemcpyHostToDevice, cs));
+        SVO_HIP(hipMemcpyAsync(dhp, has_point, (size_t)T, hipMemcpyHostToDevice, cs));
         spx = dpx; sbr = dbr; spt = dpt; shp = dhp;
     }
+    SVO_HIP(hipEventRecord(c->staged, cs));
+    SVO_HIP(hipStreamWaitEvent(s, c->staged, 0));
+    SVO_HIP(hipMemcpyAsync(b->d_pairs + first, d_desc, sizeof(svo::PairDesc) * count, hipMemcpyDeviceToDevice, s));
     if (T > 0)
         hipLaunchKernelGGL(scatter_features_kernel, dim3(count), dim3(256), 0, s, d_off, spx, sbr, spt, shp, b->d_px,
                            b->d_bearing, b->d_point, b->d_has_point, first, b->max_f);
     SVO_HIP(hipGetLastError());
-    // the offsets and descriptors are read from host memory this call owns: wait for them
-    SVO_HIP(hipStreamSynchronize(s));
+    SVO_HIP(hipEventRecord(c->stage_free, s));
+    // the offsets, descriptors and (host) features are read from memory the caller and this call own:
+    // wait for the upload only; the scatter stays queued on `stream` behind earlier work
+    SVO_HIP(hipStreamSynchronize(cs));
     for (int32_t i = 0; i < count; ++i) b->pair_set[first + i] = 1;
     return SVO_OK;
 }
