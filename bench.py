@@ -138,7 +138,10 @@ def main():
     if args.cpu_rehearsal:
         return rehearsal(args, rank, world, dist)
 
-    ctx = svo_amd.Context(local_rank)
+    # SVO_BENCH_SHARED_GPU=1: every rank on device 0 (a rehearsal of the N > 1 path on a one-GPU box; the
+    # line then says so and its value is not a scaling number)
+    shared_gpu = os.environ.get("SVO_BENCH_SHARED_GPU") == "1"
+    ctx = svo_amd.Context(0 if shared_gpu else local_rank)
     P, nf, L, patch = args.pairs, args.features, args.levels, args.patch
     D = max(1, min(args.distinct, P))
     nthreads = max(1, min(16, os.cpu_count() or 1))
@@ -278,7 +281,8 @@ def main():
                                f"patch {patch}, {L}-level pyramid, {cam['width']}x{cam['height']}, {P} pairs/GPU",
                    "pairs_per_gpu": P, "features": nf, "levels": L, "patch": patch, "distinct_scenes": D,
                    "feature_order": args.feature_order,
-                   "parallelism": f"pairs sharded over {world} GPU(s), no collective"},
+                   "parallelism": f"pairs sharded over {world} GPU(s), no collective"
+                                  + (" (rehearsal: every rank on device 0)" if shared_gpu else "")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": f"align chain: {L} levels x (K1 residual [+ pair init at the first level], K2 robust scale, "
