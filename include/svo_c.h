@@ -153,7 +153,10 @@ int svo_align_batch_set_pair(svo_align_batch* batch, int32_t pair, const svo_pyr
  *   px, bearing, point, has_point: the pairs' feature rows packed pair after pair (pair i's rows start at
  *   the sum of the earlier pairs' n_ref + n_kf), layouts as set_pair.  With features_on_device != 0 they
  *   are device pointers on the context's device (e.g. FeatureSelection output), else host memory.
- * Synchronous: every host array is consumed and the copies are complete on return. */
+ * Every host array is consumed on return; the upload runs on a copy stream of the context (overlapping
+ * earlier work queued there, e.g. a pyramid build) and the scatter is queued on the context stream,
+ * ordered before any later work on it.  With features_on_device the call also waits for the scatter, so
+ * the device arrays may be reused on return. */
 int svo_align_batch_set_pairs(svo_align_batch* batch, int32_t first, int32_t count, const svo_pyramid_set* ref_set,
                               const svo_pyramid_set* kf_set, const svo_pyramid_set* cur_set, const int32_t* frames,
                               const double* poses, const int32_t* n_feat, const double* px, const double* bearing,

@@ -628,8 +628,10 @@ int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, 
     SVO_HIP(hipGetLastError());
     SVO_HIP(hipEventRecord(c->stage_free, s));
     // the offsets, descriptors and (host) features are read from memory the caller and this call own:
-    // wait for the upload only; the scatter stays queued on `stream` behind earlier work
+    // wait for the upload only; the scatter stays queued on `stream` behind earlier work (device features:
+    // the caller's arrays are read by the scatter itself, so wait for it too)
     SVO_HIP(hipStreamSynchronize(cs));
+    if (features_on_device && T > 0) SVO_HIP(hipStreamSynchronize(s));
     for (int32_t i = 0; i < count; ++i) b->pair_set[first + i] = 1;
     return SVO_OK;
 }

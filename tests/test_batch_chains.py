@@ -86,12 +86,19 @@ def test_gpu_two_chain_batch(mode):
         p1, e1, s1 = b1.results()
         assert np.array_equal(p1[0], poses[i]) and e1[0] == err[i] and s1[0] == st[i], i
         b1.close()
-    # the bulk form: the same batch from one svo_align_batch_set_pairs call (and one of 2 calls)
-    for split in (P, 57):
+    # the bulk form: the same batch from one svo_align_batch_set_pairs call (and one of 2 calls), with the
+    # features in host memory (uploaded on the context's copy stream) or on the device (torch tensors)
+    for split, on_dev in ((P, False), (57, False), (P, True)):
         bb = svo_amd.AlignBatch(cam, PATCH, 0, L - 1, P, NF, ctx, median_mode=mode)
         for lo in range(0, P, split):
             hi = min(P, lo + split)
-            bb.set_pairs(lo, ps, ps, ps, *packed(sc, range(lo, hi)))
+            args = packed(sc, range(lo, hi))
+            if on_dev:
+                import torch
+                feats = [torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0") for a in args[3:]]
+                torch.cuda.synchronize()
+                args = (*args[:3], *feats)
+            bb.set_pairs(lo, ps, ps, ps, *args)
         bb.run()
         pb, eb, sb = bb.results()
         assert np.array_equal(pb, poses) and np.array_equal(eb, err) and np.array_equal(sb, st)
