@@ -508,7 +508,9 @@ struct RefSel {
             nbase = nf & ~(kBlk - 1);
         }
         const bool copy = dst != where;
-        double* const mbp = where == kLds ? sh.mb : gmb;
+        // the LDS mailbox whenever the round's Ks swaps fit it (global rounds included: their values still
+        // come from and go to global storage, but the exchange skips a global store / load pair)
+        double* const mbp = (where == kLds || ks <= kCap / 2) ? sh.mb : gmb;
         // ---- sources to the mailbox: right side kept -> L_k's value at k - 1; left side kept -> R_k's.
         // Two blocks per pass: their loads are in flight together, then stored.
         for (uint32_t b = first_own(b0); b <= b1; b += 2 * kRW) {
