@@ -1,7 +1,7 @@
 """CPU: the occupancy budgets the reference-mode throughput depends on, read from the
 built gfx950 code object (tools/kernel_resources.py).  K2R's 8-wave instantiation must keep two workgroups
 per CU: at most 128 VGPRs per lane (2 workgroups x 8 waves = 4 waves per SIMD) and at most 80 KB of LDS;
-a change that crossed 128 VGPRs halved the headline (67.7k against 89.2k pairs/s).  The 16-wave
+a change that crossed 128 VGPRs cut the headline from 89.2k to 67.7k pairs/s.  The 16-wave
 instantiation runs one workgroup per CU: 128 VGPRs (4 waves per SIMD) and at most 160 KB."""
 import os
 import sys
