@@ -19,7 +19,7 @@ for step in "$@"; do
     case "$step" in
         smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
         quick) run quick 300 python3 tests/gpu_smoke.py ;;
-        tests) run tests 900 python3 -m pytest tests -q -m gpu -p no:cacheprovider ;;
+        tests) run tests 900 python3 -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bench) run bench 600 python3 bench.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu ;;
         pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-secondary --core-only
