@@ -177,13 +177,23 @@ int svo_align_batch_results(svo_align_batch* batch, double* poses, double* err, 
 /* Per-level records of one pair (max_level+1 entries, indexed by level). */
 int svo_align_batch_traces(svo_align_batch* batch, int32_t pair, svo_level_trace* out);
 
+/* Device forms of the reference robust scale (SVO_MEDIAN_REFERENCE): K2V keeps the residual vector in
+ * registers (vectors of <= 50 176 slots: config 2's 2000 features x 25), K2R runs its large rounds through
+ * global scratch (any size).  Both give the same bits. */
+enum { SVO_SCALE_AUTO = 0, SVO_SCALE_K2R = 1, SVO_SCALE_K2V = 2 };
+
 /* Diagnostics (no reference counterpart): the SVO_MEDIAN_REFERENCE robust scale of an arbitrary residual
  * vector, i.e. algorithm::computeMAD(values, n_valid) (src/algorithm.cpp:855-865) and the median it uses, on
- * the device.  values: n_slots doubles, none NaN (an invisible slot is DBL_MAX); med_mad[0] = median,
- * med_mad[1] = MAD.  Synchronous.  With the environment variable SVO_DEBUG_STAMPS set, med_mad must hold
- * 206 doubles: [2..9] cycles / block rounds / one-wave rounds / heap select per pass, [10..189] the block
- * rounds (segment size, where it lived, cycles), [190..205] cycles per round phase (tools/k2r_probe.py). */
-int svo_debug_robust_scale(svo_ctx* ctx, const double* values, int64_t n_slots, int64_t n_valid, double* med_mad);
+ * the device, with the kernel `impl` (SVO_SCALE_*; AUTO picks K2V where the vector fits).  values: n_slots
+ * doubles, none NaN (an invisible slot is DBL_MAX).  out[0] = median, out[1] = MAD, then as many diagnostics
+ * as out_len allows (out_len >= 2):
+ *   K2V: [2 + 5p ..] per pass p: cycles, block rounds, one-wave rounds, heap select, chunked exchanges;
+ *   K2R: with the environment variable SVO_DEBUG_STAMPS set, [2..9] cycles / block rounds / one-wave rounds
+ *        / heap select per pass, [10..189] the block rounds, [190..205] cycles per round phase
+ *        (tools/k2r_probe.py).
+ * Synchronous.  SVO_ERR_ARG if impl is K2V and the vector does not fit it. */
+int svo_debug_robust_scale(svo_ctx* ctx, const double* values, int64_t n_slots, int64_t n_valid, int32_t impl,
+                           double* out, int64_t out_len);
 
 /* ---------------------------------------------------------------- FeatureAlignment
  * Replaces FeatureAlignment::align(refFeature, curFrame, pixelPos) (src/feature_alignment.cpp:25-62,

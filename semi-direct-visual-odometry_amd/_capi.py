@@ -76,7 +76,7 @@ _SIGNATURES = [
     ("svo_align_batch_profile", c_int32, [c_void_p, ctypes.POINTER(ctypes.c_float)]),
     ("svo_align_batch_results", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     ("svo_align_batch_traces", c_int32, [c_void_p, c_int32, c_void_p]),
-    ("svo_debug_robust_scale", c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, c_void_p]),
+    ("svo_debug_robust_scale", c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, c_int32, c_void_p, ctypes.c_int64]),
     ("svo_feature_align", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_int32,
                                     c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("svo_feature_align_multi", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_void_p,

@@ -774,14 +774,21 @@ class FeatureSelection:
         return self._emit(frame, px, resp, n.value)
 
 
-def debug_robust_scale(values, n_valid, ctx=None):
+SCALE_AUTO, SCALE_K2R, SCALE_K2V = 0, 1, 2  # include/svo_c.h SVO_SCALE_*
+SCALE_K2V_MAX_SLOTS = 98 * 512              # K2V holds the vector in registers (align_refv.hip)
+
+
+def debug_robust_scale(values, n_valid, ctx=None, impl=SCALE_AUTO, diagnostics=False):
     """svo_debug_robust_scale: algorithm::computeMAD(values, n_valid) with the reference's libstdc++
-    nth_element post-state (MEDIAN_REFERENCE), on the device; returns (median, mad).  values: the full
-    residual vector, invisible slots = DBL_MAX (src/optimizer.cpp:387-396)."""
+    nth_element post-state (MEDIAN_REFERENCE), on the device with kernel `impl` (SCALE_*); returns (median,
+    mad), or (median, mad, diagnostics) with diagnostics=True (the 204 doubles after them, see
+    include/svo_c.h).  values: the full residual vector, invisible slots = DBL_MAX (src/optimizer.cpp:387-396)."""
     ctx = ctx or default_context()
     v = np.ascontiguousarray(values, np.float64)
-    out = np.zeros(2)
-    check(lib().svo_debug_robust_scale(ctx.handle, ptr(v), len(v), int(n_valid), ptr(out)))
+    out = np.zeros(206)
+    check(lib().svo_debug_robust_scale(ctx.handle, ptr(v), len(v), int(n_valid), int(impl), ptr(out), len(out)))
+    if diagnostics:
+        return float(out[0]), float(out[1]), out[2:].copy()
     return float(out[0]), float(out[1])
 
 

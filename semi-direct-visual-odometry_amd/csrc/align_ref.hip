@@ -35,10 +35,13 @@
 #include "svo_internal.h"
 #include "svo_math.h"
 #include "svo_wave.h"
+#include "ref_common.h"
 
 namespace svo {
 
 namespace {
+
+using namespace refsel;
 
 constexpr uint32_t kBlk = 512;               // positions per block (8 steps of 64), owned by wave block % TW
 // TW waves per pair: 8 (512 threads, two pairs per CU: batches of more than 128 pairs per launch) or 16
@@ -49,11 +52,8 @@ struct Geo {
     static constexpr uint32_t Cap = (TW == 8 ? 9u : 20u) * kBlk;  // LDS segment capacity (block-aligned base)
 };
 constexpr uint32_t kRecSteps = 1024;         // LDS step records (absolute steps): vectors of <= 64512 slots
-constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr double kDblMax = 1.7976931348623157e308;
 constexpr int kLogCap = 60;                  // diagnostics: block rounds logged per call
 
-enum { kSrc = 0, kGlb = 1, kLds = 2 };  // where the current segment lives
 
 template <int NB, int TW>
 struct RefShared {
@@ -78,99 +78,11 @@ struct Diag {  // svo_debug_robust_scale diagnostics (compiled out of the produc
     uint64_t ph[2][8];  // cycles per phase of the block rounds (thread 0), [global, LDS]
 };
 
-__device__ __forceinline__ int lg2(uint32_t n) { return 31 - __builtin_clz(n); }
-__device__ __forceinline__ uint64_t low_mask(uint32_t b) { return b >= 64 ? ~0ull : ((1ull << b) - 1ull); }
-__device__ __forceinline__ uint32_t popc(uint64_t m) { return (uint32_t)__popcll(m); }
-// position of the j-th (0-based) set bit of m
-__device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t j) {
-    uint32_t pos = 0;
-#pragma unroll
-    for (int w = 32; w >= 1; w >>= 1) {
-        const uint32_t c = popc(m & ((1ull << w) - 1ull));
-        if (j >= c) { j -= c; m >>= w; pos += (uint32_t)w; }
-    }
-    return pos;
-}
-// block-uniform values loaded or computed in vector registers, moved to scalar registers (control flow on
-// them stays scalar)
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-__device__ __forceinline__ uint64_t uni(uint64_t v) { return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v); }
-__device__ __forceinline__ double uni(double v) { return __builtin_bit_cast(double, uni(__builtin_bit_cast(uint64_t, v))); }
-__device__ __forceinline__ uint64_t lane_read64(uint64_t v, int l) {
-    return ((uint64_t)lane_read((uint32_t)(v >> 32), l) << 32) | lane_read((uint32_t)v, l);
-}
 __device__ __forceinline__ double bperm(double v, uint32_t src_lane) {
     const uint2 u = __builtin_bit_cast(uint2, v);
     const int a = (int)(src_lane * 4u);
     return __builtin_bit_cast(double, make_uint2((uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)u.x),
                                                  (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)u.y)));
-}
-
-// libstdc++ __move_median_to_first(result, a, b, c): the chosen position and value
-__device__ __forceinline__ void median3(double a, double b, double c, uint32_t A, uint32_t B, uint32_t C, uint32_t& ch,
-                                        double& p) {
-    if (a < b) {
-        if (b < c) { ch = B; p = b; }
-        else if (a < c) { ch = C; p = c; }
-        else { ch = A; p = a; }
-    } else if (a < c) { ch = A; p = a; }
-    else if (b < c) { ch = C; p = c; }
-    else { ch = B; p = b; }
-}
-
-// ---- heap select (depth limit), one lane: stl_heap.h __adjust_heap / __push_heap / __make_heap /
-// __pop_heap and stl_algo.h __heap_select restated over positions first + i, then the swap of first and nth
-// (tests/cpp/introselect_model.cpp checks the restatement).  Only adversarial inputs reach it; a free
-// function of plain values, so that the selection state never needs an address.
-__device__ __attribute__((noinline)) void heap_select_fn(double* seg, uint32_t base, double* gseg, int where, uint32_t first,
-                                                         uint32_t len, uint32_t middle, uint32_t nth_rel) {
-    auto get = [&](uint32_t i) { return where == kLds ? seg[first + i - base] : gseg[first + i]; };
-    auto put = [&](uint32_t i, double v) {
-        if (where == kLds) seg[first + i - base] = v;
-        else gseg[first + i] = v;
-    };
-    auto push_heap = [&](uint32_t hole, uint32_t top, double value) {
-        uint32_t parent = (hole - 1) / 2;
-        while (hole > top && get(parent) < value) {
-            put(hole, get(parent));
-            hole = parent;
-            parent = (hole - 1) / 2;
-        }
-        put(hole, value);
-    };
-    auto adjust_heap = [&](uint32_t hole, uint32_t n, double value) {
-        const uint32_t top = hole;
-        uint32_t second = hole;
-        while (n >= 1 && second < (n - 1) / 2) {
-            second = 2 * (second + 1);
-            if (get(second) < get(second - 1)) second--;
-            put(hole, get(second));
-            hole = second;
-        }
-        if ((n & 1u) == 0 && second == (n - 2) / 2) {
-            second = 2 * (second + 1);
-            put(hole, get(second - 1));
-            hole = second - 1;
-        }
-        push_heap(hole, top, value);
-    };
-    if (middle >= 2) {
-        uint32_t parent = (middle - 2) / 2;
-        while (true) {
-            adjust_heap(parent, middle, get(parent));
-            if (parent == 0) break;
-            parent--;
-        }
-    }
-    for (uint32_t i = middle; i < len; ++i)
-        if (get(i) < get(0)) {
-            const double v = get(i);
-            put(i, get(0));
-            adjust_heap(0, middle, v);
-        }
-    const double f0 = get(0), n0 = get(nth_rel);  // std::iter_swap(first, nth)
-    put(0, n0);
-    put(nth_rel, f0);
 }
 
 // NB: rows of 64 blocks held in registers by the block scans (2: M <= 64512, 17: M <= 524288).  With NB = 2
@@ -888,7 +800,17 @@ int64_t ref_sel_stride(int64_t max_slots) {
     const int64_t mp = (max_slots + kBlk - 1) / kBlk * kBlk + kBlk;
     return 4 * mp;
 }
+// SVO_SCALE_IMPL (measurement knob, read once): 2 selects K2V where the vector fits its registers
+// (<= refv_max_slots() slots); default K2R (until K2V's per-pair latency beats K2R's two pairs per CU)
+int scale_impl() {
+    static const int v = getenv("SVO_SCALE_IMPL") ? atoi(getenv("SVO_SCALE_IMPL")) : 0;
+    return v;
+}
 void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s) {
+    if (scale_impl() == SVO_SCALE_K2V && (int64_t)a.max_f * a.area <= refv_max_slots()) {
+        launch_scale_refv(a, level, s);
+        return;
+    }
     // a launch of at most 128 pairs (small batches, one pair per frame) gives each pair a whole CU
     const bool wide = a.n_pairs <= 128;
     const bool small = (int64_t)a.max_f * a.area <= (int64_t)kSmallM;
@@ -897,8 +819,14 @@ void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s) {
     else if (wide) hipLaunchKernelGGL((align_scale_ref_kernel<17, 16>), dim3(a.n_pairs), dim3(Geo<16>::RT), 0, s, a, level);
     else hipLaunchKernelGGL((align_scale_ref_kernel<17, 8>), dim3(a.n_pairs), dim3(Geo<8>::RT), 0, s, a, level);
 }
-void launch_debug_robust_scale(const double* v, uint32_t M, uint32_t n, uint32_t* sel, int64_t sel_stride, double* out,
-                               hipStream_t s) {
+int launch_debug_robust_scale(const double* v, uint32_t M, uint32_t n, uint32_t* sel, int64_t sel_stride, int impl,
+                              double* out, hipStream_t s) {
+    if (impl == SVO_SCALE_AUTO) impl = M <= (uint32_t)refv_max_slots() ? SVO_SCALE_K2V : SVO_SCALE_K2R;
+    if (impl == SVO_SCALE_K2V) {
+        if (M > (uint32_t)refv_max_slots()) return -1;
+        launch_debug_robust_scale_v(v, M, n, reinterpret_cast<double*>(sel), out, s);
+        return 0;
+    }
     // (SVO_K2R_WAVES=16: the 16-wave instantiation, as small batches run it)
     static const bool w16 = getenv("SVO_K2R_WAVES") && atoi(getenv("SVO_K2R_WAVES")) == 16;
     if (M <= kSmallM) {
@@ -908,6 +836,7 @@ void launch_debug_robust_scale(const double* v, uint32_t M, uint32_t n, uint32_t
         if (w16) hipLaunchKernelGGL((debug_robust_scale_kernel<17, 16>), dim3(1), dim3(Geo<16>::RT), 0, s, v, M, n, sel, sel_stride, out);
         else hipLaunchKernelGGL((debug_robust_scale_kernel<17, 8>), dim3(1), dim3(Geo<8>::RT), 0, s, v, M, n, sel, sel_stride, out);
     }
+    return 0;
 }
 
 }  // namespace svo

@@ -1,0 +1,811 @@
+// align_refv.hip — K2V: the reference's robust scale bit for bit with the residual vector resident in
+// registers (median_mode SVO_MEDIAN_REFERENCE, vectors of up to kVCap slots; K2R in align_ref.hip takes
+// larger ones).
+//
+// What it reproduces: Optimizer::tukeyWeighting (src/optimizer.cpp:485-514) takes sigma = 1.4826 * MAD with
+// algorithm::computeMedian (src/algorithm.cpp:834-853) on the FULL residual vector (n_features * patch^2
+// slots, feature-major, invisible slots = DBL_MAX): std::nth_element(vec, vec + n/2), then for an even total
+// length (vec[n/2 - 1] + vec[n/2]) / 2 with vec[n/2 - 1] as libstdc++'s introselect left it; the MAD is the
+// same call on |r_i - median| in the original order (:855-865).  The rounds are the parallel Hoare rounds of
+// tests/cpp/introselect_model.cpp (checked there against the real std::nth_element):
+//   median of three (first+1, first+S/2, last-1) moved to first, pivot p;
+//   GE = positions in (first, last) with !(a < p), LE = positions in [first, last) with !(p < a);
+//   the k-th GE from the left (L_k) and the k-th LE from the right (R_k) swap for k <= Ks,
+//   Ks = max over split points t of min(#GE before t, #LE from t on); cut = min(L_{Ks+1}, R_{Ks}).
+//
+// Why registers.  A pair's vector is 50 000 doubles (400 KB) at config 2: more than the 160 KB of LDS, so
+// K2R ran its large rounds through global scratch (three sweeps of the segment per round, ~6 MB of traffic
+// per pair and level).  A CU's register file is 512 KB: one 512-thread workgroup (two waves per SIMD, 256
+// VGPRs each) holds the whole vector as R = 98 doubles per lane, and every round works on registers.
+// Position q lives in lane q % 64 of wave (q / 64) % 8, row q / 512 ("step" q / 64 = 8 row + wave), so a
+// segment [f, l) always spreads over all eight waves.  Per round:
+//   1. classify (each wave its own steps): apply the median-of-three swap in registers, GE / LE by two
+//      compares per step; the 64-bit masks go to LDS records;                       barrier
+//   2. every wave scans the records of [f, l) (13 steps per lane), finds the crossing and Ks, then L_{Ks+1},
+//      R_{Ks} and L_{Ks} by a counted step search + a bit select; the owners publish the pre-values the next
+//      round's pivot and vec[nth - 1] need; sources write the mailbox (LDS, k - 1);  barrier
+//   3. targets on the kept side take the mailbox values; all read the next pivot's candidates.
+// A mailbox larger than kMbCap swaps runs in chunks.  Segments of <= 512 continue on one wave from an LDS
+// copy without barriers; the depth limit falls back to the restated heap select (adversarial inputs only).
+// No global traffic but the two reads of K1's residuals per pair and level (one per pass).
+#include "svo_internal.h"
+#include "svo_math.h"
+#include "svo_wave.h"
+#include "ref_common.h"
+
+namespace svo {
+
+namespace {
+
+using namespace refsel;
+
+constexpr int kVT = 512;              // threads per pair
+constexpr int kVW = kVT / 64;         // waves
+constexpr int kVRows = 98;            // doubles per lane: vectors of <= 50 176 slots
+constexpr int kVBase = 80;            // first data VGPR (the asm blocks name v80 / v[80 + 2r])
+constexpr int kVRegRows = 88;         // rows in v80..v255; rows 88..97 in LDS (VShared::lrow)
+static_assert(kVBase + 2 * kVRegRows == 256, "register rows fill v80..v255");
+constexpr uint32_t kVCap = (uint32_t)kVRows * kVT;
+constexpr uint32_t kMbCap = 12288;    // mailbox (doubles); Ks beyond it exchanges in chunks
+constexpr uint32_t kOneWave = 512;    // segments of <= 512 positions continue on wave 0
+
+template <int R>
+struct VShared {
+    static constexpr int kSteps = R * kVW;
+    double mb[kMbCap];                // mailbox; the one-wave segment (mb[0, 512)) and its mailbox (mb[512, 768))
+    uint4 rec[kSteps];                // per step of the round: GE lo, GE hi, LE lo, LE hi
+    uint32_t cnt[kSteps];             // per step: #GE | #LE << 16
+    uint32_t pre[kSteps];             // per step: #GE | #LE << 16 before it (each wave writes its own steps)
+    double pub[6];                    // pre-values published by their owners (candidates 0-3, record 4)
+    double bcd;                       // broadcast of the median between the passes
+    double dummy[64];                 // per-lane target of the branch-free stores of lanes with nothing to store
+    double lrow[R - kVRegRows][kVT];  // rows 88..97 of the vector (the rest is in registers)
+    uint32_t tmp[2 * kVW];            // per-wave counts of the prologue
+};
+
+struct VDiag {  // svo_debug_robust_scale diagnostics
+    uint32_t nblock[2], nwave[2], heap[2], nchunk[2];
+    uint64_t cyc[2];
+    uint64_t ph[8];  // thread 0's cycles per phase, both passes: load, classify, barrier 1, scan + searches,
+                     // sources, barrier 2, targets, exits (dump, one-wave rounds, final)
+};
+// a phase stamp of the debug kernel (compiled out of the product kernel: dg is a null constant there)
+#define VSTAMP(i) \
+    do { \
+        if (dg && tid == 0) { const uint64_t t_ = clock64(); dg->ph[i] += t_ - tstamp; tstamp = t_; } \
+    } while (0)
+
+// The vector in registers.  Row r < 88 (positions 512 r + tid) of every lane lives in the VGPR pair
+// v[80 + 2r : 81 + 2r] (v80..v255), outside the values the compiler allocates; rows 88..97 live in LDS.  The
+// rows are loaded by one asm block (buffer loads straight into the pairs) and read / written by a
+// block-uniform index in VGPR indexing mode (s_set_gpr_idx_on + v_mov).  The compiler's own code must stay in
+// v0..v79: tools/check_vreg_fence.py checks the generated assembly at every build (the Makefile fails
+// otherwise).  Left to the compiler, 98 register-resident doubles plus the round logic did not fit 256
+// VGPRs: unrolled row bodies had their per-row values computed for all rows at once, and 16-double vectors
+// indexed dynamically were copied whole at control-flow joins; both spilled to scratch, and the VGPR-count
+// attribute does not cap the allocation.
+#define SVO_VROWS_ASM \
+    "v_add_u32 %[vt], 0x0, %[vo]\n\tbuffer_load_dwordx2 v[80:81], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x1000, %[vo]\n\tbuffer_load_dwordx2 v[82:83], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x2000, %[vo]\n\tbuffer_load_dwordx2 v[84:85], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x3000, %[vo]\n\tbuffer_load_dwordx2 v[86:87], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x4000, %[vo]\n\tbuffer_load_dwordx2 v[88:89], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x5000, %[vo]\n\tbuffer_load_dwordx2 v[90:91], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x6000, %[vo]\n\tbuffer_load_dwordx2 v[92:93], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x7000, %[vo]\n\tbuffer_load_dwordx2 v[94:95], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x8000, %[vo]\n\tbuffer_load_dwordx2 v[96:97], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x9000, %[vo]\n\tbuffer_load_dwordx2 v[98:99], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0xa000, %[vo]\n\tbuffer_load_dwordx2 v[100:101], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0xb000, %[vo]\n\tbuffer_load_dwordx2 v[102:103], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0xc000, %[vo]\n\tbuffer_load_dwordx2 v[104:105], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0xd000, %[vo]\n\tbuffer_load_dwordx2 v[106:107], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0xe000, %[vo]\n\tbuffer_load_dwordx2 v[108:109], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0xf000, %[vo]\n\tbuffer_load_dwordx2 v[110:111], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x10000, %[vo]\n\tbuffer_load_dwordx2 v[112:113], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x11000, %[vo]\n\tbuffer_load_dwordx2 v[114:115], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x12000, %[vo]\n\tbuffer_load_dwordx2 v[116:117], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x13000, %[vo]\n\tbuffer_load_dwordx2 v[118:119], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x14000, %[vo]\n\tbuffer_load_dwordx2 v[120:121], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x15000, %[vo]\n\tbuffer_load_dwordx2 v[122:123], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x16000, %[vo]\n\tbuffer_load_dwordx2 v[124:125], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x17000, %[vo]\n\tbuffer_load_dwordx2 v[126:127], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x18000, %[vo]\n\tbuffer_load_dwordx2 v[128:129], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x19000, %[vo]\n\tbuffer_load_dwordx2 v[130:131], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x1a000, %[vo]\n\tbuffer_load_dwordx2 v[132:133], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x1b000, %[vo]\n\tbuffer_load_dwordx2 v[134:135], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x1c000, %[vo]\n\tbuffer_load_dwordx2 v[136:137], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x1d000, %[vo]\n\tbuffer_load_dwordx2 v[138:139], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x1e000, %[vo]\n\tbuffer_load_dwordx2 v[140:141], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x1f000, %[vo]\n\tbuffer_load_dwordx2 v[142:143], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x20000, %[vo]\n\tbuffer_load_dwordx2 v[144:145], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x21000, %[vo]\n\tbuffer_load_dwordx2 v[146:147], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x22000, %[vo]\n\tbuffer_load_dwordx2 v[148:149], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x23000, %[vo]\n\tbuffer_load_dwordx2 v[150:151], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x24000, %[vo]\n\tbuffer_load_dwordx2 v[152:153], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x25000, %[vo]\n\tbuffer_load_dwordx2 v[154:155], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x26000, %[vo]\n\tbuffer_load_dwordx2 v[156:157], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x27000, %[vo]\n\tbuffer_load_dwordx2 v[158:159], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x28000, %[vo]\n\tbuffer_load_dwordx2 v[160:161], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x29000, %[vo]\n\tbuffer_load_dwordx2 v[162:163], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x2a000, %[vo]\n\tbuffer_load_dwordx2 v[164:165], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x2b000, %[vo]\n\tbuffer_load_dwordx2 v[166:167], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x2c000, %[vo]\n\tbuffer_load_dwordx2 v[168:169], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x2d000, %[vo]\n\tbuffer_load_dwordx2 v[170:171], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x2e000, %[vo]\n\tbuffer_load_dwordx2 v[172:173], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x2f000, %[vo]\n\tbuffer_load_dwordx2 v[174:175], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x30000, %[vo]\n\tbuffer_load_dwordx2 v[176:177], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x31000, %[vo]\n\tbuffer_load_dwordx2 v[178:179], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x32000, %[vo]\n\tbuffer_load_dwordx2 v[180:181], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x33000, %[vo]\n\tbuffer_load_dwordx2 v[182:183], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x34000, %[vo]\n\tbuffer_load_dwordx2 v[184:185], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x35000, %[vo]\n\tbuffer_load_dwordx2 v[186:187], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x36000, %[vo]\n\tbuffer_load_dwordx2 v[188:189], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x37000, %[vo]\n\tbuffer_load_dwordx2 v[190:191], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x38000, %[vo]\n\tbuffer_load_dwordx2 v[192:193], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x39000, %[vo]\n\tbuffer_load_dwordx2 v[194:195], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x3a000, %[vo]\n\tbuffer_load_dwordx2 v[196:197], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x3b000, %[vo]\n\tbuffer_load_dwordx2 v[198:199], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x3c000, %[vo]\n\tbuffer_load_dwordx2 v[200:201], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x3d000, %[vo]\n\tbuffer_load_dwordx2 v[202:203], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x3e000, %[vo]\n\tbuffer_load_dwordx2 v[204:205], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x3f000, %[vo]\n\tbuffer_load_dwordx2 v[206:207], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x40000, %[vo]\n\tbuffer_load_dwordx2 v[208:209], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x41000, %[vo]\n\tbuffer_load_dwordx2 v[210:211], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x42000, %[vo]\n\tbuffer_load_dwordx2 v[212:213], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x43000, %[vo]\n\tbuffer_load_dwordx2 v[214:215], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x44000, %[vo]\n\tbuffer_load_dwordx2 v[216:217], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x45000, %[vo]\n\tbuffer_load_dwordx2 v[218:219], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x46000, %[vo]\n\tbuffer_load_dwordx2 v[220:221], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x47000, %[vo]\n\tbuffer_load_dwordx2 v[222:223], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x48000, %[vo]\n\tbuffer_load_dwordx2 v[224:225], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x49000, %[vo]\n\tbuffer_load_dwordx2 v[226:227], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x4a000, %[vo]\n\tbuffer_load_dwordx2 v[228:229], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x4b000, %[vo]\n\tbuffer_load_dwordx2 v[230:231], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x4c000, %[vo]\n\tbuffer_load_dwordx2 v[232:233], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x4d000, %[vo]\n\tbuffer_load_dwordx2 v[234:235], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x4e000, %[vo]\n\tbuffer_load_dwordx2 v[236:237], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x4f000, %[vo]\n\tbuffer_load_dwordx2 v[238:239], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x50000, %[vo]\n\tbuffer_load_dwordx2 v[240:241], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x51000, %[vo]\n\tbuffer_load_dwordx2 v[242:243], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x52000, %[vo]\n\tbuffer_load_dwordx2 v[244:245], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x53000, %[vo]\n\tbuffer_load_dwordx2 v[246:247], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x54000, %[vo]\n\tbuffer_load_dwordx2 v[248:249], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x55000, %[vo]\n\tbuffer_load_dwordx2 v[250:251], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x56000, %[vo]\n\tbuffer_load_dwordx2 v[252:253], %[vt], %[rs], 0 offen\n\t" \
+    "v_add_u32 %[vt], 0x57000, %[vo]\n\tbuffer_load_dwordx2 v[254:255], %[vt], %[rs], 0 offen\n\t"
+
+// the lane's value in block-uniform row r / store x there.  Index mode writes M0; M0 is reserved to the
+// compiler, which uses it nowhere in these kernels (checked with the fence).  Volatile asm keeps the row
+// accesses in program order.
+__device__ __forceinline__ double vget(int r) {
+    uint32_t lo, hi;
+    asm volatile(
+        "s_set_gpr_idx_on %2, gpr_idx(SRC0)\n\tv_mov_b32 %0, v80\n\tv_mov_b32 %1, v81\n\ts_set_gpr_idx_off"
+        : "=v"(lo), "=v"(hi)
+        : "s"(__builtin_amdgcn_readfirstlane(2 * r)));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ void vset(int r, double x) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    asm volatile(
+        "s_set_gpr_idx_on %2, gpr_idx(DST)\n\tv_mov_b32 v80, %0\n\tv_mov_b32 v81, %1\n\ts_set_gpr_idx_off"
+        :
+        : "v"((uint32_t)u), "v"((uint32_t)(u >> 32)), "s"(__builtin_amdgcn_readfirstlane(2 * r)));
+}
+// rows 0..87 of src (positions 512 r + tid) into the data VGPRs; lanes past `bytes` read 0 (buffer range)
+__device__ __forceinline__ void vload(const double* src, uint32_t bytes, int tid) {
+    const uint64_t a = (uint64_t)src;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 rs;
+    rs.x = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    rs.y = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32) & 0xFFFFu);
+    rs.z = __builtin_amdgcn_readfirstlane(bytes);
+    rs.w = 0x00020000u;  // raw buffer, gfx9 data format (ck.hpp CK_BUFFER_RESOURCE_3RD_DWORD)
+    // the whole offset in the VGPR (the buffer range check ignores soffset): lanes past `bytes` read 0
+    const uint32_t vo = (uint32_t)tid * 8u;
+    uint32_t vt;
+    asm volatile(SVO_VROWS_ASM "s_waitcnt vmcnt(0)"
+                 : [vt] "=&v"(vt)
+                 : [vo] "v"(vo), [rs] "s"(rs)
+                 : "memory", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v164", "v165", "v166", "v167", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255");
+}
+
+template <int R>
+struct VSel {
+    static_assert(R == 98, "register layout: rows 0..87 in v80..v255, 88..97 in LDS");
+    static constexpr int kSteps = R * kVW;
+    static constexpr int kKl = (kSteps + 63) / 64;  // scan entries per lane
+    VShared<R>& sh;
+    double* gseg;        // the pair's global scratch: the heap select's segment (depth limit only)
+    uint32_t gdummy;     // its per-lane dummy slots (gseg[gdummy + lane], past every position)
+    VDiag* dg;           // diagnostics (debug kernel) or nullptr
+    uint32_t M, nth;
+    int tid, lane, wave;
+    // block-uniform selection state
+    uint32_t f, l;
+    int depth;
+    bool rec;
+    double lo_val;
+    int P;
+
+    // ------------------------------------------------------------------ registers
+    // body(r, x) for this wave's rows rlo..rhi, x the lane's value (kWrite: body may change it)
+    template <bool kWrite, typename F>
+    __device__ __forceinline__ void rows(int rlo, int rhi, F&& body) {
+        const int r1 = rhi < kVRegRows - 1 ? rhi : kVRegRows - 1;
+        for (int r = rlo; r <= r1; ++r) {
+            double x = vget(r);
+            body(r, x);
+            if (kWrite) vset(r, x);
+        }
+        for (int r = rlo > kVRegRows ? rlo : kVRegRows; r <= rhi; ++r) {
+            double& y = sh.lrow[r - kVRegRows][tid];
+            double x = y;
+            body(r, x);
+            if (kWrite) y = x;
+        }
+    }
+    __device__ __forceinline__ double row_val(int r) const {
+        return r < kVRegRows ? vget(r) : sh.lrow[r - kVRegRows][tid];
+    }
+    __device__ __forceinline__ void row_set(int r, uint32_t ln, double x) {
+        if ((uint32_t)lane != ln) return;
+        if (r < kVRegRows) vset(r, x);
+        else sh.lrow[r - kVRegRows][tid] = x;
+    }
+    __device__ __forceinline__ void load(const double* src, bool mad, double med) {
+        vload(src, M * 8u, tid);  // (rows past M hold 0: never inside a segment)
+        for (int r = kVRegRows; r < R; ++r) {
+            const uint32_t q = (uint32_t)r * kVT + (uint32_t)tid;
+            sh.lrow[r - kVRegRows][tid] = q < M ? src[q] : 0.0;
+        }
+        if (mad) {  // src/algorithm.cpp:860-863 (DBL_MAX stays DBL_MAX)
+            rows<true>(0, R - 1, [&](int, double& x) __attribute__((always_inline)) { x = fabs(x - med); });
+        }
+    }
+    // this wave's rows r whose step 8 r + wave lies in [s0, s1] (rlo > rhi: none)
+    __device__ __forceinline__ void wave_rows(uint32_t s0, uint32_t s1, int& rlo, int& rhi) const {
+        const int w = wave;
+        rlo = (int)s0 <= w ? 0 : ((int)s0 - w + kVW - 1) / kVW;
+        rhi = (int)s1 < w ? -1 : ((int)s1 - w) / kVW;
+    }
+    // lanes of this wave's step in row r inside [f, l): fw = f - 64 wave, lw = l - 64 wave
+    static __device__ __forceinline__ uint64_t row_mask(int fw, int lw, int r) {
+        const int b = r * kVT;
+        const int lo = fw - b, hi = lw - b;
+        return low_mask((uint32_t)(hi < 0 ? 0 : hi)) & ~low_mask((uint32_t)(lo < 0 ? 0 : lo));
+    }
+    // the owner of position q stores its current value in pub[slot]
+    __device__ __forceinline__ void publish(uint32_t q, int slot) {
+        if (((q >> 6) & (kVW - 1)) != (uint32_t)wave) return;
+        const double x = row_val((int)(q >> 9));
+        if ((uint32_t)lane == (q & 63u)) sh.pub[slot] = x;
+    }
+    // positions [f, l) -> dst[q - dbase]; the other lanes store to dummy + lane (branch-free)
+    __device__ __forceinline__ void dump(double* dst, uint32_t dbase, double* dummy) {
+        int rlo, rhi;
+        wave_rows(f >> 6, (l - 1) >> 6, rlo, rhi);
+        const int fo = (int)f - tid, lo = (int)l - tid;  // q = 512 r + tid in [f, l)
+        double* const d = dst + ((uint32_t)tid - dbase);
+        double* const dl = dummy + lane;
+        rows<false>(rlo, rhi, [&](int r, double x) __attribute__((always_inline)) {
+            const int b = r * kVT;
+            *(b >= fo && b < lo ? d + b : dl) = x;
+        });
+    }
+
+    // ------------------------------------------------------------------ 1. classification
+    __device__ __forceinline__ void classify(double p, uint32_t ch, double x0) {
+        // std::iter_swap(first, chosen) of __move_median_to_first, in the owners' registers
+        if (((f >> 6) & (kVW - 1)) == (uint32_t)wave) row_set((int)(f >> 9), f & 63u, p);
+        if (((ch >> 6) & (kVW - 1)) == (uint32_t)wave) row_set((int)(ch >> 9), ch & 63u, x0);
+        int rlo, rhi;
+        wave_rows(f >> 6, (l - 1) >> 6, rlo, rhi);
+        const int fw = (int)f - 64 * wave, lw = (int)l - 64 * wave;
+        const int rf = ((f >> 6) & (kVW - 1)) == (uint32_t)wave ? (int)(f >> 9) : -1;
+        const uint32_t lf = f & 63u;
+        uint4* const recw = sh.rec + wave;
+        uint32_t* const cntw = sh.cnt + wave;
+        rows<false>(rlo, rhi, [&](int r, double x) __attribute__((always_inline)) {
+            const uint64_t inm = row_mask(fw, lw, r);
+            const uint64_t fb = r == rf ? 1ull << lf : 0ull;
+            const uint64_t ge = __ballot(!(x < p)) & inm & ~fb;
+            const uint64_t le = __ballot(!(p < x)) & inm;
+            if (lane == 0) {
+                recw[r * kVW] = make_uint4((uint32_t)ge, (uint32_t)(ge >> 32), (uint32_t)le, (uint32_t)(le >> 32));
+                cntw[r * kVW] = popc(ge) | (popc(le) << 16);
+            }
+        });
+    }
+
+    // ------------------------------------------------------------------ 2. scan and searches (every wave)
+    struct Scan {
+        uint32_t pk[kKl];  // exclusive #GE | #LE << 16 before entry lane * kKl + i
+        uint32_t sf, E, totG, totL;
+    };
+    __device__ __forceinline__ void scan(Scan& S) {
+        S.sf = f >> 6;
+        S.E = ((l - 1) >> 6) - S.sf + 1;
+        uint32_t tg = 0, tl = 0;
+#pragma unroll
+        for (int i = 0; i < kKl; ++i) {
+            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
+            const uint32_t c = e < S.E ? sh.cnt[S.sf + e] : 0u;
+            S.pk[i] = tg | (tl << 16);
+            tg += c & 0xFFFFu;
+            tl += c >> 16;
+        }
+        const uint32_t ig = wave_incl_scan(tg), il = wave_incl_scan(tl);
+        const uint32_t off = (ig - tg) | ((il - tl) << 16);
+#pragma unroll
+        for (int i = 0; i < kKl; ++i) {
+            S.pk[i] += off;
+            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
+            if (e < S.E && ((S.sf + e) & (kVW - 1)) == (uint32_t)wave) sh.pre[S.sf + e] = S.pk[i];
+        }
+        S.totG = uni(lane_read(ig, 63));
+        S.totL = uni(lane_read(il, 63));
+    }
+    // the packed prefix of a block-uniform entry
+    __device__ __forceinline__ uint32_t pk_at(const Scan& S, uint32_t e) const {
+        const uint32_t li = e / kKl, ii = e % kKl;
+        uint32_t x = S.pk[0];
+#pragma unroll
+        for (int i = 1; i < kKl; ++i) x = ii == (uint32_t)i ? S.pk[i] : x;
+        return uni(lane_read(x, (int)li));
+    }
+    __device__ __forceinline__ uint64_t rec_mask(uint32_t s, int kind) const {
+        const uint4 m = sh.rec[s];
+        return kind ? ((uint64_t)uni(m.w) << 32) | uni(m.z) : ((uint64_t)uni(m.y) << 32) | uni(m.x);
+    }
+    // the rank-th (1-based) GE (kind 0) or LE (kind 1) position from the left; cnt = #entries whose prefix is
+    // below the rank (so the entry cnt - 1 holds it)
+    __device__ __forceinline__ uint32_t locate(const Scan& S, uint32_t cnt, int kind, uint32_t rank) const {
+        const uint32_t e = cnt - 1u;
+        const uint32_t pk = pk_at(S, e);
+        const uint32_t pre = kind ? pk >> 16 : pk & 0xFFFFu;
+        return (S.sf + e) * 64u + select_bit(rec_mask(S.sf + e, kind), rank - pre - 1u);
+    }
+    // the rank (1-based) of position q among the round's swap targets of a side, 0 if it is none
+    // (side 0: GE ranked from the left, side 1: LE ranked from the right).  From the scan registers and the
+    // records, so it runs before the mailbox barrier: after it, a fast wave's next classification may
+    // already overwrite the records.
+    __device__ __forceinline__ uint32_t side_rank(const Scan& S, uint32_t q, int side, uint32_t ks, uint32_t totL) const {
+        const uint32_t s = q >> 6, b = q & 63u;
+        const uint64_t m = rec_mask(s, side);
+        const uint32_t pp = pk_at(S, s - S.sf);
+        if (!((m >> b) & 1ull)) return 0;
+        const uint32_t k = side ? totL - ((pp >> 16) + popc(m & low_mask(b))) : (pp & 0xFFFFu) + popc(m & low_mask(b)) + 1u;
+        return k <= ks ? k : 0u;
+    }
+
+    // ------------------------------------------------------------------ 3. the exchange
+    // side 0: GE positions ranked from the left (L_k), side 1: LE positions ranked from the right (R_k), over
+    // the steps [s0, s1]; ranks k in (k0, k1]: kWrite stores the value in mb[k - 1 - k0], else the position
+    // takes it.  The masks are recomputed from the registers (the same compares as the classification).
+    // chunked (more than one exchange chunk): the masks come from the records instead, since an earlier
+    // chunk's targets may have changed registers the recompute would read (the round then ends with a barrier,
+    // so no wave reads the records while a faster one classifies the next round)
+    template <bool kWrite>
+    __device__ __forceinline__ void exchange(int side, uint32_t s0, uint32_t s1, double p, uint32_t totL, uint32_t k0,
+                                             uint32_t k1, bool chunked) {
+        int rlo, rhi;
+        wave_rows(s0, s1, rlo, rhi);
+        if (rlo > rhi) return;
+        const int fw = (int)f - 64 * wave, lw = (int)l - 64 * wave;
+        const int rf = ((f >> 6) & (kVW - 1)) == (uint32_t)wave ? (int)(f >> 9) : -1;
+        const uint32_t lf = f & 63u;
+        // this wave's step prefixes, lane j: row j (and row 64 + j): one LDS read each, then readlanes
+        const uint32_t pre0 = sh.pre[((uint32_t)lane * kVW + (uint32_t)wave) % kSteps];
+        const uint32_t pre1 = sh.pre[(((uint32_t)lane + 64u) * kVW + (uint32_t)wave) % kSteps];
+        double* const dl = sh.dummy + lane;
+        rows<!kWrite>(rlo, rhi, [&](int r, double& x) __attribute__((always_inline)) {
+            const uint32_t pp = uni(lane_read(r < 64 ? pre0 : pre1, r & 63));
+            const uint64_t inm = row_mask(fw, lw, r);
+            uint64_t m;
+            uint32_t k;
+            if (chunked) {
+                m = rec_mask((uint32_t)(r * kVW + wave), side);
+            } else if (side == 0) {
+                const uint64_t fb = r == rf ? 1ull << lf : 0ull;
+                m = __ballot(!(x < p)) & inm & ~fb;
+            } else {
+                m = __ballot(!(p < x)) & inm;
+            }
+            if (side == 0) k = (pp & 0xFFFFu) + lanes_below(m) + 1u;
+            else k = totL - ((pp >> 16) + lanes_below(m));
+            // branch-free: lanes with nothing to exchange use their dummy slot
+            const bool ok = ((m >> lane) & 1ull) && k > k0 && k <= k1;
+            double* const a = ok ? sh.mb + (k - 1u - k0) : dl;
+            if (kWrite) {
+                *a = x;
+            } else {
+                const double t = *a;
+                x = ok ? t : x;
+            }
+        });
+    }
+
+    // ------------------------------------------------------------------ one block round
+    // pivot p (moved to f), x0 the value moved to ch; on return [f, l) is the kept side and cand[] the next
+    // round's A, B, C, first values (when another block round follows)
+    // fresh opaque copies of the thread / lane / wave numbers: values derived from them would otherwise be
+    // hoisted out of the round loop and held in registers for all of it
+    __device__ __forceinline__ void refresh_ids() {
+        asm volatile("" : "+v"(tid), "+v"(lane));
+        wave = (int)uni((uint32_t)tid >> 6);
+    }
+    __device__ __forceinline__ void block_round(double p, uint32_t ch, double x0, double (&cand)[4]) {
+        refresh_ids();
+        uint64_t tstamp = dg ? clock64() : 0;
+        classify(p, ch, x0);
+        VSTAMP(1);
+        __syncthreads();
+        VSTAMP(2);
+        Scan S;
+        scan(S);
+        const uint32_t totL = S.totL, totG = S.totG;
+        // the crossing: the last entry whose start has G < Lc (entry 0 always: G = 0 < Lc = totL)
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < kKl; ++i) {
+            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
+            if (e < S.E) c += (S.pk[i] & 0xFFFFu) < totL - (S.pk[i] >> 16) ? 1u : 0u;
+        }
+        const uint32_t es = uni(wave_sum_u(c)) - 1u;
+        const uint32_t pke = pk_at(S, es);
+        const uint32_t ks = uni(crossing_ks(pke & 0xFFFFu, totL - (pke >> 16), rec_mask(S.sf + es, 0), rec_mask(S.sf + es, 1)));
+        // L_{Ks+1} (GE rank Ks + 1), R_{Ks} (LE rank totL - Ks + 1 from the left), L_{Ks}: one packed count
+        const uint32_t ra = ks + 1u, rb = totL - ks + 1u, rc = ks;
+        c = 0;
+#pragma unroll
+        for (int i = 0; i < kKl; ++i) {
+            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
+            if (e < S.E) {
+                const uint32_t pg = S.pk[i] & 0xFFFFu, pl = S.pk[i] >> 16;
+                c += (pg < ra ? 1u : 0u) + (pl < rb ? 1u << 10 : 0u) + (pg < rc ? 1u << 20 : 0u);
+            }
+        }
+        const uint32_t cs = uni(wave_sum_u(c));
+        const uint32_t lk1 = ra <= totG ? uni(locate(S, cs & 1023u, 0, ra)) : kNone;
+        const uint32_t rk = ks >= 1 ? uni(locate(S, (cs >> 10) & 1023u, 1, rb)) : kNone;
+        const uint32_t lk = ks >= 1 ? uni(locate(S, cs >> 20, 0, rc)) : kNone;
+        const uint32_t cut = lk1 < rk ? lk1 : rk;
+        const bool right = cut <= nth;  // the side introselect continues with
+        const uint32_t nf = right ? cut : f, nl = right ? l : cut;
+        // vec[nth - 1] after this round (never touched again): only L_{Ks} can sit at cut - 1
+        const bool record = cut == nth && !rec;
+        if (record) publish(lk == cut - 1u ? rk : cut - 1u, 4);
+        const uint32_t nS = nl - nf;
+        const bool need = nS > kOneWave && depth > 0;  // another block round follows
+        const uint32_t cq[4] = {nf + 1u, nf + nS / 2u, nl - 1u, nf};
+        if (need) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) publish(cq[i], i);
+        }
+        // sources: the side the kept side takes its values from; targets: the kept side's swapped positions
+        const int src_side = right ? 0 : 1, tgt_side = right ? 1 : 0;
+        const uint32_t sl = (l - 1) >> 6;
+        const uint32_t s0L = S.sf, s1L = lk != kNone ? lk >> 6 : 0u;           // L_k, k <= Ks
+        const uint32_t s0R = rk != kNone ? rk >> 6 : sl + 1u, s1R = sl;       // R_k, k <= Ks
+        // Ks beyond the mailbox: chunks of kMbCap ranks, the masks from the records (see exchange).
+        const uint32_t nch = ks == 0 ? 1u : (ks + kMbCap - 1u) / kMbCap;
+        uint32_t ck[4] = {0, 0, 0, 0};  // the candidates' target ranks (0: not a target)
+        if (need && ks) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ck[i] = side_rank(S, cq[i], tgt_side, ks, totL);
+        }
+        VSTAMP(3);
+        for (uint32_t it = 0; it < nch; ++it) {
+            const uint32_t ci = it;
+            const uint32_t k0 = ci * kMbCap, k1 = ks < k0 + kMbCap ? ks : k0 + kMbCap;
+            if (ks) {
+                if (src_side == 0) exchange<true>(0, s0L, s1L, p, totL, k0, k1, nch > 1);
+                else exchange<true>(1, s0R, s1R, p, totL, k0, k1, nch > 1);
+            }
+            VSTAMP(4);
+            __syncthreads();
+            VSTAMP(5);
+            if (it == 0) {
+                if (record) { lo_val = uni(sh.pub[4]); rec = true; }
+                if (need) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) cand[i] = uni(sh.pub[i]);
+                }
+            }
+            if (ks) {
+                if (tgt_side == 0) exchange<false>(0, s0L, s1L, p, totL, k0, k1, nch > 1);
+                else exchange<false>(1, s0R, s1R, p, totL, k0, k1, nch > 1);
+                if (need) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        if (ck[i] > k0 && ck[i] <= k1) cand[i] = uni(sh.mb[ck[i] - 1u - k0]);
+                }
+            }
+            if (it + 1 < nch) __syncthreads();
+        }
+        if (nch > 1) __syncthreads();  // (records read above until here)
+        VSTAMP(6);
+        if (dg && tid == 0) dg->nchunk[P] += nch > 1 ? 1u : 0u;
+        f = nf;
+        l = nl;
+    }
+
+    // ------------------------------------------------------------------ rounds of <= 512 positions (wave 0)
+    // No barriers: the segment stays in LDS (seg[i] = position f0 + i), lane L of step j reads position
+    // f0 + 64 j + L each round; the candidates are broadcast reads, the masks compares, the counts / crossing
+    // / rank searches scalars, the swaps go through a mailbox (a wave's LDS accesses complete in program
+    // order).  Stops at <= 3 positions or depth 0.
+    __device__ __forceinline__ void wave_rounds(double* seg, double* mb, uint32_t& nrounds) {
+        const uint32_t f0 = f, me = (uint32_t)lane;
+        uint32_t fr = 0, lr = l - f;
+        const uint32_t nrel = nth - f0;
+        while (lr - fr > 3 && depth > 0) {
+            --depth;
+            ++nrounds;
+            const uint32_t A = fr + 1, B = fr + (lr - fr) / 2, C = lr - 1;
+            const double a = uni(seg[A]), b = uni(seg[B]), c = uni(seg[C]), xv = uni(seg[fr]);
+            uint32_t chh;
+            double pe;
+            median3(a, b, c, A, B, C, chh, pe);
+            if (me == 0) {  // std::iter_swap(first, chosen)
+                seg[fr] = pe;
+                seg[chh] = xv;
+            }
+            const uint32_t js = fr >> 6, je = (lr - 1) >> 6;
+            double w[8];
+            uint64_t ge[8], le[8];
+            uint32_t gp[8], lp[8];  // #GE / #LE before each step
+            uint32_t tG = 0, tL = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                ge[j] = le[j] = 0;
+                w[j] = 0.0;
+                if ((uint32_t)j >= js && (uint32_t)j <= je) {
+                    const uint32_t base = 64u * (uint32_t)j, i = base + me;
+                    w[j] = seg[i < lr ? i : fr];
+                    const uint32_t lo = fr > base ? (fr - base < 64u ? fr - base : 64u) : 0u;
+                    const uint32_t hi = lr > base ? (lr - base < 64u ? lr - base : 64u) : 0u;
+                    const uint64_t inm = low_mask(hi) & ~low_mask(lo);
+                    const uint64_t fb = (fr >> 6) == (uint32_t)j ? 1ull << (fr & 63u) : 0ull;
+                    ge[j] = __ballot(!(w[j] < pe)) & inm & ~fb;
+                    le[j] = __ballot(!(pe < w[j])) & inm;
+                }
+                gp[j] = tG;
+                lp[j] = tL;
+                tG += popc(ge[j]);
+                tL += popc(le[j]);
+            }
+            // crossing: the last step whose start has G < Lc (step js: G = 0 < Lc)
+            uint32_t gcar = 0, lcar = tL;
+            uint64_t a0 = 0, b0m = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if ((uint32_t)j >= js && (uint32_t)j <= je && gp[j] < tL - lp[j]) { gcar = gp[j]; lcar = tL - lp[j]; a0 = ge[j]; b0m = le[j]; }
+            const uint32_t ks = crossing_ks(gcar, lcar, a0, b0m);
+            auto rank_pos = [&](int kind, uint32_t rank) -> uint32_t {  // the last step starting below the rank
+                if (rank == 0 || rank > (kind ? tL : tG)) return kNone;
+                uint32_t pre = 0, jj = 0;
+                uint64_t mk = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const uint32_t pj = kind ? lp[j] : gp[j];
+                    if ((uint32_t)j >= js && (uint32_t)j <= je && pj < rank) { pre = pj; jj = (uint32_t)j; mk = kind ? le[j] : ge[j]; }
+                }
+                return 64u * jj + select_bit(mk, rank - pre - 1u);
+            };
+            const uint32_t lk1 = rank_pos(0, ks + 1), rk = ks >= 1 ? rank_pos(1, tL - ks + 1) : kNone;
+            const uint32_t cut = lk1 < rk ? lk1 : rk;
+            const bool right = cut <= nrel;
+            if (cut == nrel && !rec && nrel >= 1) {
+                const uint32_t lk = ks >= 1 ? rank_pos(0, ks) : kNone;
+                lo_val = uni(seg[lk == cut - 1 ? rk : cut - 1]);
+                rec = true;
+            }
+            // sources to the mailbox, then the kept side's targets take it (straight into seg)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if ((uint32_t)j < js || (uint32_t)j > je) continue;
+                const uint64_t m = right ? ge[j] : le[j];
+                const uint32_t k = right ? gp[j] + lanes_below(m) + 1u : tL - (lp[j] + lanes_below(m));
+                if (((m >> me) & 1ull) && k <= ks) mb[k - 1] = w[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if ((uint32_t)j < js || (uint32_t)j > je) continue;
+                const uint64_t m = right ? le[j] : ge[j];
+                const uint32_t k = right ? tL - (lp[j] + lanes_below(m)) : gp[j] + lanes_below(m) + 1u;
+                if (((m >> me) & 1ull) && k <= ks) seg[64u * (uint32_t)j + me] = mb[k - 1];
+            }
+            if (right) fr = cut;
+            else lr = cut;
+        }
+        f = f0 + fr;
+        l = f0 + lr;
+    }
+
+    // ------------------------------------------------------------------ std::nth_element(vec, vec + nth)
+    // (vec[nth - 1], vec[nth]) of the post-state, on thread 0
+    __device__ __forceinline__ void select(const double* src, bool mad, double med, double& hi, double& lo) {
+        const uint64_t t0 = dg ? clock64() : 0;
+        uint64_t tstamp = t0;
+        load(src, mad, med);
+        VSTAMP(0);
+        f = 0;
+        l = M;
+        depth = M > 1 ? 2 * lg2(M) : 0;
+        rec = false;
+        lo_val = 0.0;
+        double cand[4] = {0.0, 0.0, 0.0, 0.0};
+        if (M >= 4) {  // round 1's candidates straight from the source (uniform loads)
+            const uint32_t qs[4] = {1u, M / 2u, M - 1u, 0u};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const double x = src[qs[i]];
+                cand[i] = uni(mad ? fabs(x - med) : x);
+            }
+        }
+        uint32_t nblock = 0;
+        while (l - f > kOneWave && depth > 0) {
+            --depth;
+            ++nblock;
+            uint32_t ch;
+            double p;
+            median3(cand[0], cand[1], cand[2], f + 1u, f + (l - f) / 2u, l - 1u, ch, p);
+            block_round(uni(p), uni(ch), cand[3], cand);
+        }
+        tstamp = dg ? clock64() : 0;
+        __syncthreads();  // the last round's targets still read the mailbox the exits overwrite
+        if (l - f > kOneWave) {  // depth limit on a large segment: heap select in the pair's global scratch
+            dump(gseg, 0, gseg + gdummy);
+            __threadfence_block();
+            __syncthreads();
+            if (tid == 0) {
+                heap_select_at(gseg + f, l - f, nth + 1 - f, nth - f);
+                hi = gseg[nth];
+                lo = rec ? lo_val : (nth >= 1 ? gseg[nth - 1] : 0.0);
+            }
+            if (dg && tid == 0) dg->heap[P] = 1;
+        } else {
+            double* const seg = sh.mb;  // positions f0 + i
+            const uint32_t f0 = f;
+            dump(seg, f0, sh.dummy);
+            __syncthreads();
+            if (wave == 0) {
+                uint32_t nw = 0;
+                wave_rounds(seg, sh.mb + kOneWave, nw);
+                if (tid == 0) {
+                    if (l - f <= 3) {  // std::__insertion_sort of the last <= 3
+                        const uint32_t n = l - f;
+                        double t[3] = {0.0, 0.0, 0.0};
+                        for (uint32_t i = 0; i < n; ++i) t[i] = seg[f - f0 + i];
+                        sort3(t, n);
+                        hi = t[nth - f];
+                        lo = rec ? lo_val : (nth >= f + 1 ? t[nth - 1 - f] : 0.0);
+                    } else {  // depth limit
+                        heap_select_at(seg + (f - f0), l - f, nth + 1 - f, nth - f);
+                        hi = seg[nth - f0];
+                        lo = rec ? lo_val : (nth >= f0 + 1 ? seg[nth - 1 - f0] : 0.0);
+                        if (dg) dg->heap[P] = 1;
+                    }
+                    if (dg) dg->nwave[P] = nw;
+                }
+            }
+        }
+        __syncthreads();  // seg / mailbox / gseg are reused by the next pass
+        VSTAMP(7);
+        if (dg && tid == 0) {
+            dg->nblock[P] = nblock;
+            dg->cyc[P] = clock64() - t0;
+        }
+    }
+};
+
+// computeMedian / computeMAD (src/algorithm.cpp:834-865) with the reference's post-state; every thread
+// returns med and mad.  M slots, n visible.
+template <int R>
+__device__ __forceinline__ void refv_robust_scale(const double* src, VShared<R>& sh, double* gseg, VDiag* dg, uint32_t M,
+                                                  uint32_t n, double& med, double& mad) {
+    VSel<R> s{sh, gseg, (uint32_t)((M + 63u) / 64u * 64u), dg};
+    s.M = M;
+    s.nth = n / 2;
+    s.tid = (int)threadIdx.x;
+    s.lane = s.tid & 63;
+    s.wave = (int)uni((uint32_t)(s.tid >> 6));
+    const bool even = (M & 1u) == 0 && s.nth >= 1;  // mid == 0 (UB in the reference) reads vec[mid]
+    double m0 = 0.0;
+    for (int P = 0; P < 2; ++P) {  // one copy of the selection for both passes
+        s.P = P;
+        double lo = 0.0, hi = 0.0;
+        s.select(src, P == 1, m0, hi, lo);
+        if (s.tid == 0) sh.bcd = even ? (lo + hi) / 2.0 : hi;
+        __syncthreads();
+        const double r = uni(sh.bcd);
+        __syncthreads();
+        if (P == 0) m0 = r;
+        else mad = r;
+    }
+    med = m0;
+}
+
+template <int R>
+__device__ __forceinline__ void scale_refv_pair(const AlignArgs& a, VShared<R>& sh) {
+    const int pair = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    PairState& S = a.state[pair];
+    if (!S.active) return;
+    const PairDesc& P = a.pairs[pair];
+    const int nf = P.n_ref + P.n_kf;
+    const uint32_t M = (uint32_t)nf * (uint32_t)a.area;
+    const uint8_t* __restrict__ fvis = a.fvis + (int64_t)pair * a.max_f;
+    uint32_t nrv = 0, ncv = 0;
+    for (int f = tid; f < nf; f += kVT) {
+        const uint8_t v = fvis[f];
+        nrv += v & 1;
+        ncv += v >> 1;
+    }
+    nrv = wave_sum_u(nrv);
+    ncv = wave_sum_u(ncv);
+    if (lane == 0) { sh.tmp[wave] = nrv; sh.tmp[kVW + wave] = ncv; }
+    __syncthreads();
+    nrv = 0; ncv = 0;
+    for (int w = 0; w < kVW; ++w) { nrv += sh.tmp[w]; ncv += sh.tmp[kVW + w]; }
+    const uint32_t n = ncv * (uint32_t)a.area;
+    double med = kDblMax, mad = 0.0;  // n == 0: every slot is DBL_MAX in the reference
+    if (n > 0)
+        refv_robust_scale<R>(a.scratch + (int64_t)pair * a.key_stride, sh,
+                             reinterpret_cast<double*>(a.sel + (int64_t)pair * a.sel_stride), nullptr, M, n, med, mad);
+    if (tid == 0) {
+        double sigma = 1.482602218505602 * mad;
+        if (sigma <= 2.220446049250313e-16) sigma = 2.220446049250313e-16;
+        S.med = med;
+        S.mad = mad;
+        S.sigma = sigma;
+        S.c = 4.6851 * sigma;
+        S.n = n;
+        S.n_ref_vis = nrv;
+    }
+}
+
+}  // namespace
+
+// K2V: one 512-thread workgroup per pair, one pair per CU (all of its registers and 144 KB of LDS).
+__global__ void __launch_bounds__(kVT, 1) 
+align_scale_refv_kernel(AlignArgs a, int level) {
+    __shared__ VShared<kVRows> sh;
+    (void)level;
+    scale_refv_pair<kVRows>(a, sh);
+}
+
+// svo_debug_robust_scale: the same selection on an arbitrary vector (one workgroup); out[0..1] med / mad,
+// out[2..] diagnostics (rounds, chunked rounds, heap selects, cycles per pass)
+__global__ void __launch_bounds__(kVT, 1) 
+debug_robust_scale_v_kernel(const double* v, uint32_t M, uint32_t n, double* gseg, double* out) {
+    __shared__ VShared<kVRows> sh;
+    __shared__ VDiag dg;
+    if (threadIdx.x == 0) dg = VDiag{};
+    __syncthreads();
+    double med = 0.0, mad = 0.0;
+    refv_robust_scale<kVRows>(v, sh, gseg, &dg, M, n, med, mad);
+    if (threadIdx.x == 0) {
+        out[0] = med;
+        out[1] = mad;
+        for (int P = 0; P < 2; ++P) {
+            out[2 + 5 * P] = (double)dg.cyc[P];
+            out[3 + 5 * P] = (double)dg.nblock[P];
+            out[4 + 5 * P] = (double)dg.nwave[P];
+            out[5 + 5 * P] = (double)dg.heap[P];
+            out[6 + 5 * P] = (double)dg.nchunk[P];
+        }
+        for (int i = 0; i < 8; ++i) out[12 + i] = (double)dg.ph[i];
+    }
+}
+
+int64_t refv_max_slots() { return kVCap; }
+void launch_scale_refv(const AlignArgs& a, int level, hipStream_t s) {
+    hipLaunchKernelGGL(align_scale_refv_kernel, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
+}
+void launch_debug_robust_scale_v(const double* v, uint32_t M, uint32_t n, double* gseg, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(debug_robust_scale_v_kernel, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out);
+}
+
+}  // namespace svo

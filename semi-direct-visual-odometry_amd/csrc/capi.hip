@@ -704,8 +704,8 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         SVO_HIP(hipEventRecord(c->fork, c->stream));
         for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->fork, 0));
         for (int i = 0; i < ns; ++i) {
-            const int32_t p0 = i * per, cnt = i == ns - 1 ? b->n_pairs - p0 : per;
-            if (cnt <= 0) continue;
+            const int32_t p0 = i * per, cnt = i == ns - 1 ? b->n_pairs - p0 : std::min(per, b->n_pairs - p0);
+            if (cnt <= 0) break;  // (later chains would be empty too)
             if (i >= 1 && stagger > 0) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->chain_marks[i - 1][stagger], 0));
             svo::launch_align(sub_batch(a, b, p0, cnt), i == 0 ? c->stream : c->sides[i],
                               i < ns - 1 && stagger > 0 ? c->chain_marks[i] : nullptr);
@@ -770,17 +770,24 @@ int svo_align_batch_traces(svo_align_batch* b, int32_t pair, svo_level_trace* ou
     return SVO_OK;
 }
 
-int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, int64_t n_valid, double* med_mad) {
-    if (!c || !values || !med_mad) return fail(SVO_ERR_ARG, "null argument");
+int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, int64_t n_valid, int32_t impl, double* out,
+                           int64_t out_len) {
+    if (!c || !values || !out) return fail(SVO_ERR_ARG, "null argument");
+    if (out_len < 2) return fail(SVO_ERR_ARG, "out_len %lld < 2", (long long)out_len);
+    if (impl < SVO_SCALE_AUTO || impl > SVO_SCALE_K2V) return fail(SVO_ERR_ARG, "impl %d unknown", impl);
     if (n_slots < 1 || n_slots > 524288 || n_valid < 1 || n_valid > n_slots)
         return fail(SVO_ERR_ARG, "need 1 <= n_valid <= n_slots <= 524288 (got %lld, %lld)", (long long)n_valid,
+                    (long long)n_slots);
+    if (impl == SVO_SCALE_K2V && n_slots > svo::refv_max_slots())
+        return fail(SVO_ERR_ARG, "K2V holds at most %lld slots (got %lld)", (long long)svo::refv_max_slots(),
                     (long long)n_slots);
     for (int64_t i = 0; i < n_slots; ++i)
         if (std::isnan(values[i])) return fail(SVO_ERR_ARG, "value %lld is NaN", (long long)i);
     SVO_HIP(hipSetDevice(c->device));
     const int64_t sel_stride = svo::ref_sel_stride(n_slots);  // u32
     const int64_t q = (n_slots + 63) / 64 * 64;
-    const size_t bytes = (size_t)q * 8 + (size_t)sel_stride * 4 + 2048;
+    constexpr int64_t kDiag = 206;  // the diagnostics either kernel writes
+    const size_t bytes = (size_t)q * 8 + (size_t)sel_stride * 4 + kDiag * 8;
     void* base = nullptr;
     hipError_t e = ctx_scratch(c, bytes, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_debug_robust_scale: %s", hipGetErrorString(e));
@@ -788,11 +795,13 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
     double* d_v = static_cast<double*>(base);
     uint32_t* d_sel = reinterpret_cast<uint32_t*>(d_v + q);
     double* d_out = reinterpret_cast<double*>(d_sel + sel_stride);
+    SVO_HIP(hipMemsetAsync(d_out, 0, kDiag * 8, c->stream));
     SVO_HIP(hipMemcpyAsync(d_v, values, (size_t)n_slots * 8, hipMemcpyHostToDevice, c->stream));
-    svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, sel_stride, d_out, c->stream);
+    if (svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, sel_stride, impl, d_out,
+                                       c->stream) != 0)
+        return fail(SVO_ERR_ARG, "the vector does not fit the requested kernel");
     SVO_HIP(hipGetLastError());
-    // SVO_DEBUG_STAMPS: also the diagnostics (tools/k2r_probe.py): cycles per pass, round counts, block rounds
-    SVO_HIP(hipMemcpyAsync(med_mad, d_out, getenv("SVO_DEBUG_STAMPS") ? 206 * 8 : 16, hipMemcpyDeviceToHost, c->stream));
+    SVO_HIP(hipMemcpyAsync(out, d_out, (size_t)std::min<int64_t>(out_len, kDiag) * 8, hipMemcpyDeviceToHost, c->stream));
     SVO_HIP(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }

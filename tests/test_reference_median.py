@@ -1,4 +1,5 @@
-"""The reference's robust scale bit for bit: median_mode SVO_MEDIAN_REFERENCE (K2R, csrc/align_ref.hip).
+"""The reference's robust scale bit for bit: median_mode SVO_MEDIAN_REFERENCE (K2V, csrc/align_refv.hip, for
+vectors of <= 50 176 slots; K2R, csrc/align_ref.hip, for any size).
 
 algorithm::computeMedian (src/algorithm.cpp:834-853) runs std::nth_element on the full residual vector and
 reads vec[n/2 - 1] from libstdc++'s post-partition state.  K2R re-runs that introselect on the device.
@@ -6,7 +7,7 @@ reads vec[n/2 - 1] from libstdc++'s post-partition state.  K2R re-runs that intr
 CPU: tests/cpp/introselect_model.cpp — the round formulation K2R uses (counts, prefix sums, the crossing
      max-min) against the real std::nth_element, whole final arrays, including inputs that exhaust the
      depth limit (heap select).
-GPU: svo_debug_robust_scale (the K2R selection on arbitrary vectors) and whole alignments in
+GPU: svo_debug_robust_scale (the K2V and K2R selections on arbitrary vectors) and whole alignments in
      MEDIAN_REFERENCE mode against the oracle's std::nth_element (oracle median_mode 0):
        median / MAD / sigma of every vector ............. bit-exact
        per-level n_vis, status; first-level median / MAD / sigma ... bit-exact
@@ -74,14 +75,53 @@ def residual_vectors():
     return out
 
 
+IMPLS = [pytest.param(svo_amd.SCALE_K2V, id="K2V"), pytest.param(svo_amd.SCALE_K2R, id="K2R")]
+
+
+def _fits(impl, v):
+    return impl != svo_amd.SCALE_K2V or len(v) <= svo_amd.SCALE_K2V_MAX_SLOTS
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("case", residual_vectors(), ids=lambda c: c[0])
-def test_debug_robust_scale_matches_nth_element(case):
+def test_debug_robust_scale_matches_nth_element(case, impl):
     _, v = case
+    if not _fits(impl, v):
+        pytest.skip("vector larger than K2V's registers (K2R covers it)")
     n = int((v < DBL_MAX).sum())
-    med, mad = svo_amd.debug_robust_scale(v, n)
+    med, mad = svo_amd.debug_robust_scale(v, n, impl=impl)
     med_c, mad_c = oracle_med_mad(v, n)
     assert med == med_c and mad == mad_c, (med, med_c, mad, mad_c)
+
+
+@pytest.mark.gpu
+def test_debug_robust_scale_k2v_extremes():
+    """K2V at its capacity (50 176 slots: every register row and LDS row in use), a vector whose first
+    round needs a chunked exchange (Ks > the 12 288-slot mailbox: reversed order), all-invisible tails, and
+    n_valid far below the length."""
+    rng = np.random.default_rng(11)
+    cases = []
+    v = rng.normal(0, 8, svo_amd.SCALE_K2V_MAX_SLOTS)
+    v[np.repeat(rng.random(svo_amd.SCALE_K2V_MAX_SLOTS // 25 + 1) < 0.2, 25)[:len(v)]] = DBL_MAX
+    cases.append(v)
+    cases.append(np.arange(50000, 0, -1, dtype=np.float64) * 0.01)  # descending: maximal swaps per round
+    cases.append(np.concatenate([rng.normal(0, 3, 30000), np.full(20000, DBL_MAX)]))
+    w = rng.normal(0, 3, 40000)
+    w[rng.random(40000) < 0.9] = DBL_MAX
+    cases.append(w)
+    for v in cases:
+        n = int((v < DBL_MAX).sum())
+        med, mad, dg = svo_amd.debug_robust_scale(v, n, impl=svo_amd.SCALE_K2V, diagnostics=True)
+        med_c, mad_c = oracle_med_mad(v, n)
+        assert med == med_c and mad == mad_c, (len(v), n, med, med_c, mad, mad_c, dg[:10])
+    assert dg[4] + dg[9] >= 0  # (chunk counters exist)
+
+
+@pytest.mark.gpu
+def test_debug_robust_scale_k2v_rejects_large_vectors():
+    with pytest.raises(svo_amd.SvoError):
+        svo_amd.debug_robust_scale(np.zeros(svo_amd.SCALE_K2V_MAX_SLOTS + 1), 10, impl=svo_amd.SCALE_K2V)
 
 
 @pytest.mark.gpu
@@ -97,9 +137,10 @@ def test_debug_robust_scale_heap_select_path(tmp_path):
         subprocess.check_call([str(exe), "killer", str(n), str(n // 2), str(out)])
         raw = np.fromfile(out, np.float64)
         v = raw / n * 500.0 - 250.0  # order-preserving map into the residual range
-        med, mad = svo_amd.debug_robust_scale(v, len(v))
         med_c, mad_c = oracle_med_mad(v, len(v))
-        assert med == med_c and mad == mad_c, (n, med, med_c, mad, mad_c)
+        for impl in (svo_amd.SCALE_K2V, svo_amd.SCALE_K2R):
+            med, mad = svo_amd.debug_robust_scale(v, len(v), impl=impl)
+            assert med == med_c and mad == mad_c, (n, impl, med, med_c, mad, mad_c)
 
 
 def _check_ref_traces(tr_gpu, tr_cpu, min_level, max_level):
@@ -138,7 +179,7 @@ def test_debug_robust_scale_large_vectors(n_slots):
     v = rng.normal(0, 8, n_slots)
     v[rng.random(n_slots) < 0.15] = DBL_MAX
     n = int((v < DBL_MAX).sum())
-    med, mad = svo_amd.debug_robust_scale(v, n)
+    med, mad = svo_amd.debug_robust_scale(v, n, impl=svo_amd.SCALE_K2R)
     med_c, mad_c = oracle_med_mad(v, n)
     assert med == med_c and mad == mad_c, (med, med_c, mad, mad_c)
 

@@ -1,4 +1,4 @@
-"""K2R latency probe: svo_debug_robust_scale on a config-2-shaped residual vector (50 000 slots, 80 %
+"""K2R / K2V latency probe (argument: 1 K2R, 2 K2V): svo_debug_robust_scale on a config-2-shaped residual vector (50 000 slots, 80 %
 visible, sigma 8) with the kernel's diagnostics (SVO_DEBUG_STAMPS=1): cycles per pass, block / one-wave round
 counts, and per block round the segment size, where it lived (0 K1's array, 1 global scratch, 2 LDS) and its
 cycles.  The result is checked against the oracle's std::nth_element."""
@@ -11,7 +11,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
-os.environ["SVO_DEBUG_STAMPS"] = "1"
+os.environ["SVO_DEBUG_STAMPS"] = "1"  # (K2R's phase stamps; K2V always reports its counters)
 import svo_amd  # noqa: E402
 from svo_amd import _capi  # noqa: E402
 import oracle as O  # noqa: E402
@@ -22,18 +22,27 @@ v = rng.normal(0, 8, 50000)
 v[np.repeat(rng.random(2000) < 0.2, 25)] = DBL_MAX
 n = int((v < 1e300).sum())
 ctx = svo_amd.default_context()
+impl = int(sys.argv[1]) if len(sys.argv) > 1 else svo_amd.SCALE_K2R
 out = np.zeros(206)
 for _ in range(3):
-    _capi.check(_capi.lib().svo_debug_robust_scale(ctx.handle, _capi.ptr(v), len(v), n, _capi.ptr(out)))
+    _capi.check(_capi.lib().svo_debug_robust_scale(ctx.handle, _capi.ptr(v), len(v), n, impl, _capi.ptr(out), len(out)))
 t0 = time.perf_counter()
 for _ in range(20):
-    _capi.check(_capi.lib().svo_debug_robust_scale(ctx.handle, _capi.ptr(v), len(v), n, _capi.ptr(out)))
+    _capi.check(_capi.lib().svo_debug_robust_scale(ctx.handle, _capi.ptr(v), len(v), n, impl, _capi.ptr(out), len(out)))
 dt = (time.perf_counter() - t0) / 20
 med_c = O.median(v, n, 0)
 d = np.abs(v - med_c)
 d[v >= DBL_MAX] = DBL_MAX
 mad_c = O.median(d, n, 0)
 print(f"med {out[0]!r} mad {out[1]!r}  oracle {med_c!r} {mad_c!r}  match {out[0] == med_c and out[1] == mad_c}  call {dt * 1e6:.1f} us")
+if impl == svo_amd.SCALE_K2V:
+    for p in range(2):
+        cyc, nb, nl, hp, ch = out[2 + 5 * p: 7 + 5 * p]
+        print(f"K2V pass {p}: {cyc:.0f} cycles, block rounds {nb:.0f}, one-wave rounds {nl:.0f}, heap select {hp:.0f}, "
+              f"chunked exchanges {ch:.0f}")
+    names = ("load", "classify", "barrier1", "scan+search", "sources", "barrier2", "targets", "exits")
+    print("K2V cycles per phase (thread 0, both passes): " + ", ".join(f"{a} {x:.0f}" for a, x in zip(names, out[12:20])))
+    sys.exit(0)
 for p in range(2):
     cyc, nb, nl, hp = out[2 + 4 * p: 6 + 4 * p]
     print(f"pass {p}: {cyc:.0f} cycles, block rounds {nb:.0f}, one-wave rounds {nl:.0f}, heap select {hp:.0f}")
