@@ -30,9 +30,7 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
-import svo_amd  # noqa: E402  (loads libsvo_hip.so before torch can bring its own HIP runtime)
-import svo_amd.shard as shard  # noqa: E402
-import svo_amd.synth as synth  # noqa: E402
+svo_amd = shard = synth = None  # imported in main() once this process is known to be a rank (see spawn_ranks)
 
 METRIC = "frame-pair alignments/sec @2000 feats, 5-lvl pyramid; SE(3) err vs ref"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -125,7 +123,11 @@ def spawn_ranks(n):
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus))
+        sys.exit(spawn_ranks(args.gpus))  # the launcher parent never loads the HIP library
+    global svo_amd, shard, synth
+    import svo_amd  # noqa: E402  (loads libsvo_hip.so before torch can bring its own HIP runtime)
+    import svo_amd.shard as shard  # noqa: E402
+    import svo_amd.synth as synth  # noqa: E402
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -68,6 +68,8 @@ typedef struct {
  *   SVO_MEDIAN_EXACT: true order statistics ((n/2 - 1)-th and n/2-th), the robust statistic the
  *     reference means; faster (K2). */
 enum { SVO_MEDIAN_EXACT = 0, SVO_MEDIAN_REFERENCE = 1 };
+/* SVO_MEDIAN_REFERENCE: largest residual vector per pair (max_features * patch_size^2) */
+#define SVO_REF_MAX_SLOTS 524288
 
 /* ImageAlignment(patchSize, minLevel, maxLevel, numParameters=6) (include/image_alignment.hpp:18).
  * median_mode: SVO_MEDIAN_EXACT or SVO_MEDIAN_REFERENCE (above). */

@@ -293,6 +293,7 @@ def _feature_arrays(frames):
 
 
 MEDIAN_EXACT, MEDIAN_REFERENCE = 0, 1  # include/svo_c.h SVO_MEDIAN_*
+REF_MAX_SLOTS = 524288  # include/svo_c.h SVO_REF_MAX_SLOTS
 
 
 class AlignBatch:
@@ -337,8 +338,28 @@ class AlignBatch:
         count = frames.shape[0]
         poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(count, 21)
         n_feat = np.ascontiguousarray(n_feat, dtype=np.int32).reshape(count, 2)
-        on_dev = all(hasattr(a, "data_ptr") and getattr(a, "is_cuda", False) for a in (px, bearing, point, has_point))
+        arrs = (px, bearing, point, has_point)
+        cuda = [hasattr(a, "data_ptr") and getattr(a, "is_cuda", False) for a in arrs]
+        on_dev = all(cuda)
+        if any(cuda) and not on_dev:
+            raise ValueError("set_pairs: the feature arrays must be all host arrays or all CUDA tensors")
         if on_dev:
+            import torch
+            T = int(n_feat.astype(np.int64).sum())
+            for name, a, per, dt in (("px", px, 2, (torch.float64,)), ("bearing", bearing, 3, (torch.float64,)),
+                                     ("point", point, 3, (torch.float64,)),
+                                     ("has_point", has_point, 1, (torch.uint8, torch.int8, torch.bool))):
+                if a.dtype not in dt:
+                    raise TypeError(f"set_pairs: {name} is {a.dtype}, expected {' / '.join(map(str, dt))}")
+                if not a.is_contiguous():
+                    raise ValueError(f"set_pairs: {name} must be contiguous")
+                if a.device.index != self.ctx.device:
+                    raise ValueError(f"set_pairs: {name} is on {a.device}, the batch on cuda:{self.ctx.device}")
+                if a.numel() != per * T:
+                    raise ValueError(f"set_pairs: {name} has {a.numel()} elements, expected {per} x {T} rows")
+            # the scatter runs on the library's streams: whatever torch queued to produce the tensors goes first
+            for d in {a.device for a in arrs}:
+                torch.cuda.current_stream(d).synchronize()
             ptrs = [ctypes.c_void_p(a.data_ptr()) for a in (px, bearing, point, has_point)]
             keep = (px, bearing, point, has_point)
         else:
@@ -418,7 +439,10 @@ class ImageAlignment:
         if self._batch is None or self._batch_key != key or self._batch_cap < nf:
             if self._batch is not None:
                 self._batch.close()
-            cap = max(nf, 1) if self._batch is None else max(nf, 2 * self._batch_cap)
+            grow = 1 if self._batch is None else 2 * self._batch_cap
+            if self.median_mode == MEDIAN_REFERENCE:  # doubling must not cross the reference-mode limit
+                grow = min(grow, REF_MAX_SLOTS // (self.patch_size * self.patch_size))
+            cap = max(nf, grow)
             self._batch = AlignBatch(cam, self.patch_size, self.min_level, self.max_level, 1, cap, self.ctx,
                                      median_mode=self.median_mode)
             self._batch_key, self._batch_cap = key, cap

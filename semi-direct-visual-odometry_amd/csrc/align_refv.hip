@@ -48,13 +48,17 @@ static_assert(kVBase + 2 * kVRegRows == 256, "register rows fill v80..v255");
 constexpr uint32_t kVCap = (uint32_t)kVRows * kVT;
 constexpr uint32_t kMbCap = 12288;    // mailbox (doubles); Ks beyond it exchanges in chunks
 constexpr uint32_t kOneWave = 512;    // segments of <= 512 positions continue on wave 0
+#if defined(SVO_STAMPS)
+constexpr int kScanGroup = 2;         // record reads the scan keeps in flight (the stamps cost registers)
+#else
+constexpr int kScanGroup = 4;
+#endif
 
 template <int R>
 struct VShared {
     static constexpr int kSteps = R * kVW;
     double mb[kMbCap];                // mailbox; the one-wave segment (mb[0, 512)) and its mailbox (mb[512, 768))
     uint4 rec[kSteps];                // per step of the round: GE lo, GE hi, LE lo, LE hi
-    uint32_t cnt[kSteps];             // per step: #GE | #LE << 16
     uint32_t pre[kSteps];             // per step: #GE | #LE << 16 before it (each wave writes its own steps)
     double pub[6];                    // pre-values published by their owners (candidates 0-3, record 4)
     double bcd;                       // broadcast of the median between the passes
@@ -66,14 +70,23 @@ struct VShared {
 struct VDiag {  // svo_debug_robust_scale diagnostics
     uint32_t nblock[2], nwave[2], heap[2], nchunk[2];
     uint64_t cyc[2];
-    uint64_t ph[8];  // thread 0's cycles per phase, both passes: load, classify, barrier 1, scan + searches,
-                     // sources, barrier 2, targets, exits (dump, one-wave rounds, final)
+    uint64_t ph[12];  // thread 0's cycles per phase, both passes: load, classify, barrier 1, publish + side
+                      // ranks, sources, barrier 2, targets, exits (dump, one-wave rounds, final), scan, crossing,
+                      // searches
 };
-// a phase stamp of the debug kernel (compiled out of the product kernel: dg is a null constant there)
+// a phase stamp of the debug kernel in the diagnostic build (make stamps: -DSVO_STAMPS, build/stamps/); in the
+// regular build the stamps are compiled out (they cost the debug kernel registers below the VGPR fence)
+#if defined(SVO_STAMPS)
 #define VSTAMP(i) \
     do { \
         if (dg && tid == 0) { const uint64_t t_ = clock64(); dg->ph[i] += t_ - tstamp; tstamp = t_; } \
     } while (0)
+#else
+#define VSTAMP(i) \
+    do { \
+        (void)tstamp; \
+    } while (0)
+#endif
 
 // The vector in registers.  Row r < 88 (positions 512 r + tid) of every lane lives in the VGPR pair
 // v[80 + 2r : 81 + 2r] (v80..v255), outside the values the compiler allocates; rows 88..97 live in LDS.  The
@@ -192,6 +205,94 @@ __device__ __forceinline__ void vset(int r, double x) {
         :
         : "v"((uint32_t)u), "v"((uint32_t)(u >> 32)), "s"(__builtin_amdgcn_readfirstlane(2 * r)));
 }
+// the row compares straight on the data registers (SRC0 indexed; no copy): ge = !(x < p), le = !(p < x)
+__device__ __forceinline__ void vcmp2(int r, double p, uint64_t& ge, uint64_t& le) {
+    asm volatile(
+        "s_set_gpr_idx_on %2, gpr_idx(SRC0)\n\tv_cmp_nlt_f64 %0, v[80:81], %3\n\tv_cmp_ngt_f64 %1, v[80:81], %3\n\t"
+        "s_set_gpr_idx_off"
+        : "=&s"(ge), "=&s"(le)
+        : "s"(__builtin_amdgcn_readfirstlane(2 * r)), "s"(p));
+}
+__device__ __forceinline__ uint64_t vcmp_ge(int r, double p) {
+    uint64_t m;
+    asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_cmp_nlt_f64 %0, v[80:81], %2\n\ts_set_gpr_idx_off"
+                 : "=s"(m)
+                 : "s"(__builtin_amdgcn_readfirstlane(2 * r)), "s"(p));
+    return m;
+}
+__device__ __forceinline__ uint64_t vcmp_le(int r, double p) {
+    uint64_t m;
+    asm volatile("s_set_gpr_idx_on %1, gpr_idx(SRC0)\n\tv_cmp_ngt_f64 %0, v[80:81], %2\n\ts_set_gpr_idx_off"
+                 : "=s"(m)
+                 : "s"(__builtin_amdgcn_readfirstlane(2 * r)), "s"(p));
+    return m;
+}
+// the lanes of m take x in row r (DST and SRC0 indexed: the register itself is the kept value)
+__device__ __forceinline__ void vsel(int r, double x, uint64_t m) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, x);
+    asm volatile(
+        "s_set_gpr_idx_on %3, gpr_idx(SRC0,DST)\n\tv_cndmask_b32 v80, v80, %0, %2\n\tv_cndmask_b32 v81, v81, %1, %2\n\t"
+        "s_set_gpr_idx_off"
+        :
+        : "v"((uint32_t)u), "v"((uint32_t)(u >> 32)), "s"(m), "s"(__builtin_amdgcn_readfirstlane(2 * r)));
+}
+// four consecutive rows r..r+3 (r + 3 < 88) in one index session: independent compares / moves / selects, so
+// their latencies overlap (a row at a time, a round spent ~200 cycles per row on dependent chains)
+__device__ __forceinline__ void vcmp2x4(int r, double p, uint64_t (&ge)[4], uint64_t (&le)[4]) {
+    asm volatile(
+        "s_set_gpr_idx_on %8, gpr_idx(SRC0)\n\t"
+        "v_cmp_nlt_f64 %0, v[80:81], %9\n\tv_cmp_ngt_f64 %1, v[80:81], %9\n\t"
+        "v_cmp_nlt_f64 %2, v[82:83], %9\n\tv_cmp_ngt_f64 %3, v[82:83], %9\n\t"
+        "v_cmp_nlt_f64 %4, v[84:85], %9\n\tv_cmp_ngt_f64 %5, v[84:85], %9\n\t"
+        "v_cmp_nlt_f64 %6, v[86:87], %9\n\tv_cmp_ngt_f64 %7, v[86:87], %9\n\t"
+        "s_set_gpr_idx_off"
+        : "=&s"(ge[0]), "=&s"(le[0]), "=&s"(ge[1]), "=&s"(le[1]), "=&s"(ge[2]), "=&s"(le[2]), "=&s"(ge[3]), "=&s"(le[3])
+        : "s"(__builtin_amdgcn_readfirstlane(2 * r)), "s"(p));
+}
+// kind 0: ge = !(x < p); kind 1: le = !(p < x)
+template <int kKind>
+__device__ __forceinline__ void vcmpx4(int r, double p, uint64_t (&m)[4]) {
+    if constexpr (kKind == 0)
+        asm volatile(
+            "s_set_gpr_idx_on %4, gpr_idx(SRC0)\n\tv_cmp_nlt_f64 %0, v[80:81], %5\n\tv_cmp_nlt_f64 %1, v[82:83], %5\n\t"
+            "v_cmp_nlt_f64 %2, v[84:85], %5\n\tv_cmp_nlt_f64 %3, v[86:87], %5\n\ts_set_gpr_idx_off"
+            : "=&s"(m[0]), "=&s"(m[1]), "=&s"(m[2]), "=&s"(m[3])
+            : "s"(__builtin_amdgcn_readfirstlane(2 * r)), "s"(p));
+    else
+        asm volatile(
+            "s_set_gpr_idx_on %4, gpr_idx(SRC0)\n\tv_cmp_ngt_f64 %0, v[80:81], %5\n\tv_cmp_ngt_f64 %1, v[82:83], %5\n\t"
+            "v_cmp_ngt_f64 %2, v[84:85], %5\n\tv_cmp_ngt_f64 %3, v[86:87], %5\n\ts_set_gpr_idx_off"
+            : "=&s"(m[0]), "=&s"(m[1]), "=&s"(m[2]), "=&s"(m[3])
+            : "s"(__builtin_amdgcn_readfirstlane(2 * r)), "s"(p));
+}
+__device__ __forceinline__ void vgetx4(int r, double (&x)[4]) {
+    uint32_t a0, a1, a2, a3, a4, a5, a6, a7;
+    asm volatile(
+        "s_set_gpr_idx_on %8, gpr_idx(SRC0)\n\tv_mov_b32 %0, v80\n\tv_mov_b32 %1, v81\n\tv_mov_b32 %2, v82\n\t"
+        "v_mov_b32 %3, v83\n\tv_mov_b32 %4, v84\n\tv_mov_b32 %5, v85\n\tv_mov_b32 %6, v86\n\tv_mov_b32 %7, v87\n\t"
+        "s_set_gpr_idx_off"
+        : "=v"(a0), "=v"(a1), "=v"(a2), "=v"(a3), "=v"(a4), "=v"(a5), "=v"(a6), "=v"(a7)
+        : "s"(__builtin_amdgcn_readfirstlane(2 * r)));
+    x[0] = __builtin_bit_cast(double, ((uint64_t)a1 << 32) | a0);
+    x[1] = __builtin_bit_cast(double, ((uint64_t)a3 << 32) | a2);
+    x[2] = __builtin_bit_cast(double, ((uint64_t)a5 << 32) | a4);
+    x[3] = __builtin_bit_cast(double, ((uint64_t)a7 << 32) | a6);
+}
+__device__ __forceinline__ void vselx4(int r, const double (&x)[4], const uint64_t (&m)[4]) {
+    const uint64_t u0 = __builtin_bit_cast(uint64_t, x[0]), u1 = __builtin_bit_cast(uint64_t, x[1]);
+    const uint64_t u2 = __builtin_bit_cast(uint64_t, x[2]), u3 = __builtin_bit_cast(uint64_t, x[3]);
+    asm volatile(
+        "s_set_gpr_idx_on %12, gpr_idx(SRC0,DST)\n\t"
+        "v_cndmask_b32 v80, v80, %0, %8\n\tv_cndmask_b32 v81, v81, %1, %8\n\t"
+        "v_cndmask_b32 v82, v82, %2, %9\n\tv_cndmask_b32 v83, v83, %3, %9\n\t"
+        "v_cndmask_b32 v84, v84, %4, %10\n\tv_cndmask_b32 v85, v85, %5, %10\n\t"
+        "v_cndmask_b32 v86, v86, %6, %11\n\tv_cndmask_b32 v87, v87, %7, %11\n\t"
+        "s_set_gpr_idx_off"
+        :
+        : "v"((uint32_t)u0), "v"((uint32_t)(u0 >> 32)), "v"((uint32_t)u1), "v"((uint32_t)(u1 >> 32)),
+          "v"((uint32_t)u2), "v"((uint32_t)(u2 >> 32)), "v"((uint32_t)u3), "v"((uint32_t)(u3 >> 32)),
+          "s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(__builtin_amdgcn_readfirstlane(2 * r)));
+}
 // rows 0..87 of src (positions 512 r + tid) into the data VGPRs; lanes past `bytes` read 0 (buffer range)
 __device__ __forceinline__ void vload(const double* src, uint32_t bytes, int tid) {
     const uint64_t a = (uint64_t)src;
@@ -295,60 +396,97 @@ struct VSel {
     }
 
     // ------------------------------------------------------------------ 1. classification
+    // This wave's rows of [f, l): only the first and the last can be partial; the first also drops position
+    // f (the pivot) from GE.  Interior rows take full masks without any per-row mask arithmetic.
+    struct WaveRows {
+        int rlo, rhi;
+        uint64_t ge_first, le_first, last;
+        __device__ __forceinline__ uint64_t ge(int r) const { return r == rlo ? ge_first : (r == rhi ? last : ~0ull); }
+        __device__ __forceinline__ uint64_t le(int r) const { return r == rlo ? le_first : (r == rhi ? last : ~0ull); }
+    };
+    __device__ __forceinline__ WaveRows wave_segment(uint32_t s0, uint32_t s1) const {
+        WaveRows w;
+        wave_rows(s0, s1, w.rlo, w.rhi);
+        const int fw = (int)f - 64 * wave, lw = (int)l - 64 * wave;
+        w.le_first = row_mask(fw, lw, w.rlo);
+        w.last = row_mask(fw, lw, w.rhi);
+        const bool own_f = ((f >> 6) & (kVW - 1)) == (uint32_t)wave && (int)(f >> 9) == w.rlo;
+        w.ge_first = w.le_first & ~(own_f ? 1ull << (f & 63u) : 0ull);
+        return w;
+    }
     __device__ __forceinline__ void classify(double p, uint32_t ch, double x0) {
         // std::iter_swap(first, chosen) of __move_median_to_first, in the owners' registers
         if (((f >> 6) & (kVW - 1)) == (uint32_t)wave) row_set((int)(f >> 9), f & 63u, p);
         if (((ch >> 6) & (kVW - 1)) == (uint32_t)wave) row_set((int)(ch >> 9), ch & 63u, x0);
-        int rlo, rhi;
-        wave_rows(f >> 6, (l - 1) >> 6, rlo, rhi);
-        const int fw = (int)f - 64 * wave, lw = (int)l - 64 * wave;
-        const int rf = ((f >> 6) & (kVW - 1)) == (uint32_t)wave ? (int)(f >> 9) : -1;
-        const uint32_t lf = f & 63u;
+        const WaveRows w = wave_segment(f >> 6, (l - 1) >> 6);
         uint4* const recw = sh.rec + wave;
-        uint32_t* const cntw = sh.cnt + wave;
-        rows<false>(rlo, rhi, [&](int r, double x) __attribute__((always_inline)) {
-            const uint64_t inm = row_mask(fw, lw, r);
-            const uint64_t fb = r == rf ? 1ull << lf : 0ull;
-            const uint64_t ge = __ballot(!(x < p)) & inm & ~fb;
-            const uint64_t le = __ballot(!(p < x)) & inm;
-            if (lane == 0) {
-                recw[r * kVW] = make_uint4((uint32_t)ge, (uint32_t)(ge >> 32), (uint32_t)le, (uint32_t)(le >> 32));
-                cntw[r * kVW] = popc(ge) | (popc(le) << 16);
-            }
-        });
+        auto put = [&](int r, uint64_t ge, uint64_t le) __attribute__((always_inline)) {
+            ge &= w.ge(r);
+            le &= w.le(r);
+            if (lane == 0) recw[r * kVW] = make_uint4((uint32_t)ge, (uint32_t)(ge >> 32), (uint32_t)le, (uint32_t)(le >> 32));
+        };
+        const int r1 = w.rhi < kVRegRows - 1 ? w.rhi : kVRegRows - 1;
+        int r = w.rlo;
+        for (; r + 3 <= r1; r += 4) {
+            uint64_t ge[4], le[4];
+            vcmp2x4(r, p, ge, le);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) put(r + j, ge[j], le[j]);
+        }
+        for (; r <= r1; ++r) {
+            uint64_t ge, le;
+            vcmp2(r, p, ge, le);
+            put(r, ge, le);
+        }
+        for (int r = w.rlo > kVRegRows ? w.rlo : kVRegRows; r <= w.rhi; ++r) {
+            const double x = sh.lrow[r - kVRegRows][tid];
+            put(r, __ballot(!(x < p)), __ballot(!(p < x)));
+        }
     }
 
     // ------------------------------------------------------------------ 2. scan and searches (every wave)
     struct Scan {
-        uint32_t pk[kKl];  // exclusive #GE | #LE << 16 before entry lane * kKl + i
-        uint32_t sf, E, totG, totL;
+        uint32_t pk[kKl];  // exclusive #GE | #LE << 16 before entry lane * K + i (i < K)
+        uint32_t sf, E, K, totG, totL;  // K = ceil(E / 64) entries per lane: small segments scan 1-2
     };
     __device__ __forceinline__ void scan(Scan& S) {
         S.sf = f >> 6;
         S.E = ((l - 1) >> 6) - S.sf + 1;
+        S.K = (S.E + 63u) >> 6;
         uint32_t tg = 0, tl = 0;
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
-            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
-            const uint32_t c = e < S.E ? sh.cnt[S.sf + e] : 0u;
-            S.pk[i] = tg | (tl << 16);
-            tg += c & 0xFFFFu;
-            tl += c >> 16;
+            S.pk[i] = 0;
+            if ((uint32_t)i < S.K) {
+                const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
+                uint32_t cg = 0, cl = 0;
+                if (e < S.E) {
+                    const uint4 m = sh.rec[S.sf + e];
+                    cg = (uint32_t)__popc(m.x) + (uint32_t)__popc(m.y);
+                    cl = (uint32_t)__popc(m.z) + (uint32_t)__popc(m.w);
+                }
+                S.pk[i] = tg | (tl << 16);
+                tg += cg;
+                tl += cl;
+                if ((i & (kScanGroup - 1)) == kScanGroup - 1) asm volatile("" ::: "memory");  // bounded reads in flight
+            }
         }
         const uint32_t ig = wave_incl_scan(tg), il = wave_incl_scan(tl);
         const uint32_t off = (ig - tg) | ((il - tl) << 16);
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
-            S.pk[i] += off;
-            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
-            if (e < S.E && ((S.sf + e) & (kVW - 1)) == (uint32_t)wave) sh.pre[S.sf + e] = S.pk[i];
+            if ((uint32_t)i < S.K) {
+                S.pk[i] += off;
+                const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
+                if (e < S.E && ((S.sf + e) & (kVW - 1)) == (uint32_t)wave) sh.pre[S.sf + e] = S.pk[i];
+            }
         }
         S.totG = uni(lane_read(ig, 63));
         S.totL = uni(lane_read(il, 63));
     }
     // the packed prefix of a block-uniform entry
     __device__ __forceinline__ uint32_t pk_at(const Scan& S, uint32_t e) const {
-        const uint32_t li = e / kKl, ii = e % kKl;
+        const uint32_t li = e / S.K, ii = e - li * S.K;
         uint32_t x = S.pk[0];
 #pragma unroll
         for (int i = 1; i < kKl; ++i) x = ii == (uint32_t)i ? S.pk[i] : x;
@@ -364,7 +502,23 @@ struct VSel {
         const uint32_t e = cnt - 1u;
         const uint32_t pk = pk_at(S, e);
         const uint32_t pre = kind ? pk >> 16 : pk & 0xFFFFu;
-        return (S.sf + e) * 64u + select_bit(rec_mask(S.sf + e, kind), rank - pre - 1u);
+        return (S.sf + e) * 64u + wave_select_bit(rec_mask(S.sf + e, kind), rank - pre - 1u);
+    }
+    // the j-th (0-based) set bit of a uniform mask: the lane holding it has j set bits below it
+    __device__ __forceinline__ uint32_t wave_select_bit(uint64_t m, uint32_t j) const {
+        const uint64_t hit = __ballot(((m >> lane) & 1ull) && lanes_below(m) == j);
+        return (uint32_t)__builtin_ctzll(hit);
+    }
+    // Ks from the crossing entry (see refsel::crossing_ks): lane b tests the split point after bit b
+    __device__ __forceinline__ uint32_t wave_crossing_ks(uint32_t gcar, uint32_t lcar, uint64_t ge, uint64_t le) const {
+        const uint32_t me = (uint32_t)lane;
+        const uint32_t g = gcar + lanes_below(ge) + (uint32_t)((ge >> me) & 1ull);
+        const uint32_t lc = lcar - (lanes_below(le) + (uint32_t)((le >> me) & 1ull));
+        const uint64_t q = __ballot(g >= lc);
+        const uint32_t lo = q ? (uint32_t)__builtin_ctzll(q) + 1u : 64u;  // smallest split b in [1, 64] with G >= Lc
+        const uint32_t g1 = gcar + popc(ge & low_mask(lo - 1));
+        const uint32_t l2 = lcar - popc(le & low_mask(lo));
+        return g1 > l2 ? g1 : l2;
     }
     // the rank (1-based) of position q among the round's swap targets of a side, 0 if it is none
     // (side 0: GE ranked from the left, side 1: LE ranked from the right).  From the scan registers and the
@@ -389,41 +543,81 @@ struct VSel {
     template <bool kWrite>
     __device__ __forceinline__ void exchange(int side, uint32_t s0, uint32_t s1, double p, uint32_t totL, uint32_t k0,
                                              uint32_t k1, bool chunked) {
-        int rlo, rhi;
-        wave_rows(s0, s1, rlo, rhi);
-        if (rlo > rhi) return;
-        const int fw = (int)f - 64 * wave, lw = (int)l - 64 * wave;
-        const int rf = ((f >> 6) & (kVW - 1)) == (uint32_t)wave ? (int)(f >> 9) : -1;
-        const uint32_t lf = f & 63u;
+        const WaveRows w = wave_segment(s0, s1);
+        if (w.rlo > w.rhi) return;
         // this wave's step prefixes, lane j: row j (and row 64 + j): one LDS read each, then readlanes
         const uint32_t pre0 = sh.pre[((uint32_t)lane * kVW + (uint32_t)wave) % kSteps];
         const uint32_t pre1 = sh.pre[(((uint32_t)lane + 64u) * kVW + (uint32_t)wave) % kSteps];
         double* const dl = sh.dummy + lane;
-        rows<!kWrite>(rlo, rhi, [&](int r, double& x) __attribute__((always_inline)) {
+        // the row's mailbox slots: the lanes of m ranked k0 < k <= k1 (okm) use mb[k - 1 - k0], the others
+        // their dummy slot.  Branch-free: the range test is one unsigned compare, okm its ballot and m.
+        const uint32_t nk = k1 - k0;
+        auto slot = [&](int r, uint64_t m, uint64_t& okm) __attribute__((always_inline)) -> double* {
             const uint32_t pp = uni(lane_read(r < 64 ? pre0 : pre1, r & 63));
-            const uint64_t inm = row_mask(fw, lw, r);
-            uint64_t m;
-            uint32_t k;
+            const uint32_t k = side == 0 ? (pp & 0xFFFFu) + lanes_below(m) + 1u : totL - ((pp >> 16) + lanes_below(m));
+            const uint32_t kk = k - 1u - k0;
+            okm = m & __ballot(kk < nk);
+            return ((okm >> lane) & 1ull) ? sh.mb + kk : dl;
+        };
+        auto mask = [&](int r, double x, bool reg) __attribute__((always_inline)) -> uint64_t {
+            if (chunked) return rec_mask((uint32_t)(r * kVW + wave), side);
+            if (side == 0) return (reg ? vcmp_ge(r, p) : __ballot(!(x < p))) & w.ge(r);
+            return (reg ? vcmp_le(r, p) : __ballot(!(p < x))) & w.le(r);
+        };
+        // register rows, four per iteration (independent chains: their compares, ranks and LDS accesses
+        // overlap), then the rest one at a time
+        const int r1 = w.rhi < kVRegRows - 1 ? w.rhi : kVRegRows - 1;
+        int r = w.rlo;
+        for (; r + 3 <= r1; r += 4) {
+            uint64_t m[4];
             if (chunked) {
-                m = rec_mask((uint32_t)(r * kVW + wave), side);
-            } else if (side == 0) {
-                const uint64_t fb = r == rf ? 1ull << lf : 0ull;
-                m = __ballot(!(x < p)) & inm & ~fb;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m[j] = rec_mask((uint32_t)((r + j) * kVW + wave), side);
             } else {
-                m = __ballot(!(p < x)) & inm;
+                if (side == 0) vcmpx4<0>(r, p, m);
+                else vcmpx4<1>(r, p, m);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) m[j] &= side == 0 ? w.ge(r + j) : w.le(r + j);
             }
-            if (side == 0) k = (pp & 0xFFFFu) + lanes_below(m) + 1u;
-            else k = totL - ((pp >> 16) + lanes_below(m));
-            // branch-free: lanes with nothing to exchange use their dummy slot
-            const bool ok = ((m >> lane) & 1ull) && k > k0 && k <= k1;
-            double* const a = ok ? sh.mb + (k - 1u - k0) : dl;
+            uint64_t okm[4];
+            double* a[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = slot(r + j, m[j], okm[j]);
+            if (kWrite) {
+                double x[4];
+                vgetx4(r, x);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) *a[j] = x[j];
+            } else {
+                double t[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) t[j] = *a[j];
+                vselx4(r, t, okm);
+            }
+        }
+        for (; r <= r1; ++r) {
+            uint64_t okm;
+            double* const a0 = slot(r, mask(r, 0.0, true), okm);
+            if (kWrite) {
+                *a0 = vget(r);
+            } else {
+                const double t0 = *a0;
+                vsel(r, t0, okm);
+            }
+        }
+        // LDS rows
+        for (int r = w.rlo > kVRegRows ? w.rlo : kVRegRows; r <= w.rhi; ++r) {
+            double& y = sh.lrow[r - kVRegRows][tid];
+            const double x = y;
+            uint64_t okm;
+            double* const a = slot(r, mask(r, x, false), okm);
             if (kWrite) {
                 *a = x;
             } else {
                 const double t = *a;
-                x = ok ? t : x;
+                y = ((okm >> lane) & 1ull) ? t : x;
             }
-        });
+        }
     }
 
     // ------------------------------------------------------------------ one block round
@@ -444,24 +638,26 @@ struct VSel {
         VSTAMP(2);
         Scan S;
         scan(S);
+        VSTAMP(8);
         const uint32_t totL = S.totL, totG = S.totG;
         // the crossing: the last entry whose start has G < Lc (entry 0 always: G = 0 < Lc = totL)
         uint32_t c = 0;
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
-            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
-            if (e < S.E) c += (S.pk[i] & 0xFFFFu) < totL - (S.pk[i] >> 16) ? 1u : 0u;
+            const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
+            if ((uint32_t)i < S.K && e < S.E) c += (S.pk[i] & 0xFFFFu) < totL - (S.pk[i] >> 16) ? 1u : 0u;
         }
         const uint32_t es = uni(wave_sum_u(c)) - 1u;
         const uint32_t pke = pk_at(S, es);
-        const uint32_t ks = uni(crossing_ks(pke & 0xFFFFu, totL - (pke >> 16), rec_mask(S.sf + es, 0), rec_mask(S.sf + es, 1)));
+        const uint32_t ks = uni(wave_crossing_ks(pke & 0xFFFFu, totL - (pke >> 16), rec_mask(S.sf + es, 0), rec_mask(S.sf + es, 1)));
+        VSTAMP(9);
         // L_{Ks+1} (GE rank Ks + 1), R_{Ks} (LE rank totL - Ks + 1 from the left), L_{Ks}: one packed count
         const uint32_t ra = ks + 1u, rb = totL - ks + 1u, rc = ks;
         c = 0;
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
-            const uint32_t e = (uint32_t)lane * kKl + (uint32_t)i;
-            if (e < S.E) {
+            const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
+            if ((uint32_t)i < S.K && e < S.E) {
                 const uint32_t pg = S.pk[i] & 0xFFFFu, pl = S.pk[i] >> 16;
                 c += (pg < ra ? 1u : 0u) + (pl < rb ? 1u << 10 : 0u) + (pg < rc ? 1u << 20 : 0u);
             }
@@ -471,6 +667,7 @@ struct VSel {
         const uint32_t rk = ks >= 1 ? uni(locate(S, (cs >> 10) & 1023u, 1, rb)) : kNone;
         const uint32_t lk = ks >= 1 ? uni(locate(S, cs >> 20, 0, rc)) : kNone;
         const uint32_t cut = lk1 < rk ? lk1 : rk;
+        VSTAMP(10);
         const bool right = cut <= nth;  // the side introselect continues with
         const uint32_t nf = right ? cut : f, nl = right ? l : cut;
         // vec[nth - 1] after this round (never touched again): only L_{Ks} can sit at cut - 1
@@ -796,7 +993,7 @@ debug_robust_scale_v_kernel(const double* v, uint32_t M, uint32_t n, double* gse
             out[5 + 5 * P] = (double)dg.heap[P];
             out[6 + 5 * P] = (double)dg.nchunk[P];
         }
-        for (int i = 0; i < 8; ++i) out[12 + i] = (double)dg.ph[i];
+        for (int i = 0; i < 12; ++i) out[12 + i] = (double)dg.ph[i];
     }
 }
 

@@ -370,8 +370,9 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
                     prm->median_mode);
     const int half = prm->patch_size / 2, area = (2 * half + 1) * (2 * half + 1);
     if ((int64_t)max_features * area >= (1ll << 31)) return fail(SVO_ERR_ARG, "max_features too large");
-    if (prm->median_mode == SVO_MEDIAN_REFERENCE && (int64_t)max_features * area > 524288)
-        return fail(SVO_ERR_ARG, "median_mode 1 supports up to 524288 residual slots per pair (max_features * patch^2)");
+    if (prm->median_mode == SVO_MEDIAN_REFERENCE && (int64_t)max_features * area > SVO_REF_MAX_SLOTS)
+        return fail(SVO_ERR_ARG, "median_mode 1 supports up to %d residual slots per pair (max_features * patch^2)",
+                    SVO_REF_MAX_SLOTS);
     SVO_HIP(hipSetDevice(c->device));
     svo_align_batch* b = new (std::nothrow) svo_align_batch{};
     if (!b) return fail(SVO_ERR_ARG, "out of host memory");
@@ -584,7 +585,9 @@ int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, 
     const size_t host_bytes = features_on_device ? 0 : (size_t)T * 65 + 4 * 256;
     const size_t need = off_bytes + desc_bytes + host_bytes;
     if (need > b->stage_bytes) {
-        if (b->d_stage) {  // a scatter queued on the stream may still read the old block
+        if (b->d_stage) {  // a scatter queued on the stream, or an upload left on the copy stream by an
+                           // earlier call's error exit, may still touch the old block
+            SVO_HIP(hipStreamSynchronize(b->ctx->copy));
             SVO_HIP(hipStreamSynchronize(b->ctx->stream));
             SVO_HIP(hipFree(b->d_stage));
         }

@@ -104,7 +104,10 @@ double ImageAlignment::align(std::shared_ptr<Frame>& refFrame, std::shared_ptr<F
     if (!same_cam || nr + nk > m_batchCap) {  // grow-only: a new batch only for a larger frame or another camera
         if (m_batch) svo_align_batch_destroy(m_batch);
         m_batch = nullptr;
-        const int32_t cap = std::max(nr + nk, same_cam ? 2 * m_batchCap : 1);
+        int32_t grow = same_cam ? 2 * m_batchCap : 1;
+        if (m_params.median_mode == SVO_MEDIAN_REFERENCE)  // doubling must not cross the reference-mode limit
+            grow = std::min(grow, SVO_REF_MAX_SLOTS / (m_params.patch_size * m_params.patch_size));
+        const int32_t cap = std::max(nr + nk, grow);
         check(svo_align_batch_create(m_ctx.get(), &cam, &m_params, 1, cap, &m_batch));
         m_batchCap = cap;
         m_batchCam = cam;

@@ -40,8 +40,9 @@ if impl == svo_amd.SCALE_K2V:
         cyc, nb, nl, hp, ch = out[2 + 5 * p: 7 + 5 * p]
         print(f"K2V pass {p}: {cyc:.0f} cycles, block rounds {nb:.0f}, one-wave rounds {nl:.0f}, heap select {hp:.0f}, "
               f"chunked exchanges {ch:.0f}")
-    names = ("load", "classify", "barrier1", "scan+search", "sources", "barrier2", "targets", "exits")
-    print("K2V cycles per phase (thread 0, both passes): " + ", ".join(f"{a} {x:.0f}" for a, x in zip(names, out[12:20])))
+    names = ("load", "classify", "barrier1", "publish+ranks", "sources", "barrier2", "targets", "exits", "scan",
+             "crossing", "searches")
+    print("K2V cycles per phase (thread 0, both passes): " + ", ".join(f"{a} {x:.0f}" for a, x in zip(names, out[12:23])))
     sys.exit(0)
 for p in range(2):
     cyc, nb, nl, hp = out[2 + 4 * p: 6 + 4 * p]
