@@ -800,14 +800,15 @@ int64_t ref_sel_stride(int64_t max_slots) {
     const int64_t mp = (max_slots + kBlk - 1) / kBlk * kBlk + kBlk;
     return 4 * mp;
 }
-// SVO_SCALE_IMPL (measurement knob, read once): 2 selects K2V where the vector fits its registers
-// (<= refv_max_slots() slots); default K2R (until K2V's per-pair latency beats K2R's two pairs per CU)
+// SVO_SCALE_IMPL (measurement knob, read once): 0 / unset (SVO_SCALE_AUTO) runs K2V wherever the vector fits
+// its registers (<= refv_max_slots() slots; one pair per CU at 390 us per call against K2R's 643 us with two
+// per CU: 110.5k vs 89.6k pairs/s at config 2), 1 forces K2R
 int scale_impl() {
-    static const int v = getenv("SVO_SCALE_IMPL") ? atoi(getenv("SVO_SCALE_IMPL")) : 0;
+    static const int v = getenv("SVO_SCALE_IMPL") ? atoi(getenv("SVO_SCALE_IMPL")) : SVO_SCALE_AUTO;
     return v;
 }
 void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s) {
-    if (scale_impl() == SVO_SCALE_K2V && (int64_t)a.max_f * a.area <= refv_max_slots()) {
+    if (scale_impl() != SVO_SCALE_K2R && (int64_t)a.max_f * a.area <= refv_max_slots()) {
         launch_scale_refv(a, level, s);
         return;
     }

@@ -73,6 +73,8 @@ struct VDiag {  // svo_debug_robust_scale diagnostics
     uint64_t ph[12];  // thread 0's cycles per phase, both passes: load, classify, barrier 1, publish + side
                       // ranks, sources, barrier 2, targets, exits (dump, one-wave rounds, final), scan, crossing,
                       // searches
+    uint32_t nlog;    // (stamps build) per block round: segment size and thread 0's cycles
+    uint32_t log[64][2];
 };
 // a phase stamp of the debug kernel in the diagnostic build (make stamps: -DSVO_STAMPS, build/stamps/); in the
 // regular build the stamps are compiled out (they cost the debug kernel registers below the VGPR fence)
@@ -632,6 +634,10 @@ struct VSel {
     __device__ __forceinline__ void block_round(double p, uint32_t ch, double x0, double (&cand)[4]) {
         refresh_ids();
         uint64_t tstamp = dg ? clock64() : 0;
+#if defined(SVO_STAMPS)
+        const uint64_t tround = tstamp;
+        const uint32_t S0 = l - f;
+#endif
         classify(p, ch, x0);
         VSTAMP(1);
         __syncthreads();
@@ -724,6 +730,13 @@ struct VSel {
         if (nch > 1) __syncthreads();  // (records read above until here)
         VSTAMP(6);
         if (dg && tid == 0) dg->nchunk[P] += nch > 1 ? 1u : 0u;
+#if defined(SVO_STAMPS)
+        if (dg && tid == 0 && dg->nlog < 64) {
+            dg->log[dg->nlog][0] = S0;
+            dg->log[dg->nlog][1] = (uint32_t)(clock64() - tround);
+            ++dg->nlog;
+        }
+#endif
         f = nf;
         l = nl;
     }
@@ -994,6 +1007,7 @@ debug_robust_scale_v_kernel(const double* v, uint32_t M, uint32_t n, double* gse
             out[6 + 5 * P] = (double)dg.nchunk[P];
         }
         for (int i = 0; i < 12; ++i) out[12 + i] = (double)dg.ph[i];
+        for (int i = 0; i < 128; ++i) out[24 + i] = i / 2 < (int)dg.nlog ? (double)dg.log[i / 2][i % 2] : -1.0;
     }
 }
 

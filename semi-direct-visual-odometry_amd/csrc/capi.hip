@@ -73,6 +73,7 @@ struct svo_ctx {
     size_t scratch_bytes = 0;
     // pinned host staging of the same calls (fixed size, ctx_pinned): one H2D and one D2H copy per call
     void* pinned = nullptr;
+    void* pinned_dev = nullptr;  // the same block as the device addresses it (stage_copy)
     size_t pinned_bytes = 0;
     // svo_align_batch_set_pair stages into the same block as a ring without waiting for its copies;
     // every other user of the block first drains them (ctx_pinned)
@@ -102,9 +103,11 @@ static hipError_t ctx_scratch(svo_ctx* c, size_t bytes, void** out) {
 constexpr size_t kPinnedCap = (size_t)8 << 20;
 static hipError_t ctx_pinned_alloc(svo_ctx* c) {
     if (c->pinned) return hipSuccess;
-    const hipError_t e = hipHostMalloc(&c->pinned, kPinnedCap, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&c->pinned, kPinnedCap, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&c->pinned_dev, c->pinned, 0);
     if (e != hipSuccess) {
-        c->pinned = nullptr;
+        if (c->pinned) (void)hipHostFree(c->pinned);
+        c->pinned = c->pinned_dev = nullptr;
         return e;
     }
     c->pinned_bytes = kPinnedCap;
@@ -122,16 +125,50 @@ static hipError_t ctx_ring_drain(svo_ctx* c) {
 static hipError_t ctx_pinned(svo_ctx* c, size_t bytes, void** out) {
     if (bytes > kPinnedCap) return hipErrorInvalidValue;
     if (hipError_t e = ctx_ring_drain(c)) return e;
-    if (!c->pinned) {
-        const hipError_t e = hipHostMalloc(&c->pinned, kPinnedCap, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            c->pinned = nullptr;
-            return e;
-        }
-        c->pinned_bytes = kPinnedCap;
-    }
+    if (hipError_t e = ctx_pinned_alloc(c)) return e;
     *out = c->pinned;
     return hipSuccess;
+}
+
+// Copies between the context's pinned block and device memory as a kernel that reads / writes the mapped
+// pinned block itself, not on a copy engine.  Measured on MI355X (tools/dev/fa_latency.py, rocprofv3 memory-copy
+// trace): once a process has run and freed a large alignment batch, every small SDMA transfer starts ~100 us
+// after it is queued, so each synchronous call paid ~200 us for its two copies (config 3 FeatureAlignment
+// 0.07 -> 0.28 ms per call, BENCH_r02 `secondary`).  A kernel copy is dispatched like the call's own kernel.
+// Copies that do not touch the pinned block (pageable memory) stay hipMemcpyAsync.
+namespace {
+__global__ void pinned_copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t bytes) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (uint64_t)gridDim.x * blockDim.x;
+    if ((((uintptr_t)dst | (uintptr_t)src) & 7u) == 0) {
+        const uint64_t n8 = bytes / 8;
+        uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+        const uint64_t* q = reinterpret_cast<const uint64_t*>(src);
+        for (uint64_t i = t; i < n8; i += nt) d[i] = q[i];
+        for (uint64_t i = n8 * 8 + t; i < bytes; i += nt) dst[i] = src[i];
+    } else {
+        for (uint64_t i = t; i < bytes; i += nt) dst[i] = src[i];
+    }
+}
+}  // namespace
+
+static bool in_pinned(const svo_ctx* c, const void* p, size_t bytes) {
+    const char* b = static_cast<const char*>(c->pinned);
+    const char* q = static_cast<const char*>(p);
+    return b && q >= b && q + bytes <= b + c->pinned_bytes;
+}
+static hipError_t stage_copy(svo_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    const bool h2d = kind == hipMemcpyHostToDevice;
+    const void* host = h2d ? src : dst;
+    if (!(kind == hipMemcpyHostToDevice || kind == hipMemcpyDeviceToHost) || !in_pinned(c, host, bytes))
+        return hipMemcpyAsync(dst, src, bytes, kind, s);
+    const ptrdiff_t off = static_cast<const char*>(host) - static_cast<const char*>(c->pinned);
+    char* hd = static_cast<char*>(c->pinned_dev) + off;
+    const uint64_t blocks = std::min<uint64_t>((bytes / 8 + 255) / 256 + 1, 1024);
+    hipLaunchKernelGGL(pinned_copy_kernel, dim3((uint32_t)blocks), dim3(256), 0, s,
+                       h2d ? static_cast<uint8_t*>(dst) : reinterpret_cast<uint8_t*>(hd),
+                       h2d ? reinterpret_cast<const uint8_t*>(hd) : static_cast<const uint8_t*>(src), (uint64_t)bytes);
+    return hipGetLastError();
 }
 
 struct svo_pyramid_set {
@@ -503,22 +540,22 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
             std::memcpy(hp + n * 16, bearing, n * 24);
             std::memcpy(hp + n * 40, point, n * 24);
             std::memcpy(hp + n * 64, has_point, n);
-            SVO_HIP(hipMemcpyAsync(b->d_px + 2 * fo, hp, n * 16, hipMemcpyHostToDevice, s));
-            SVO_HIP(hipMemcpyAsync(b->d_bearing + 3 * fo, hp + n * 16, n * 24, hipMemcpyHostToDevice, s));
-            SVO_HIP(hipMemcpyAsync(b->d_point + 3 * fo, hp + n * 40, n * 24, hipMemcpyHostToDevice, s));
-            SVO_HIP(hipMemcpyAsync(b->d_has_point + fo, hp + n * 64, n, hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_px + 2 * fo, hp, n * 16, hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_bearing + 3 * fo, hp + n * 16, n * 24, hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_point + 3 * fo, hp + n * 40, n * 24, hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_has_point + fo, hp + n * 64, n, hipMemcpyHostToDevice, s));
         }
-        SVO_HIP(hipMemcpyAsync(b->d_pairs + pair, h, sizeof(d), hipMemcpyHostToDevice, s));
+        SVO_HIP(stage_copy(c, b->d_pairs + pair, h, sizeof(d), hipMemcpyHostToDevice, s));
     } else {
         (void)hipGetLastError();
         SVO_HIP(ctx_ring_drain(c));
         if (nf > 0) {
-            SVO_HIP(hipMemcpyAsync(b->d_px + 2 * fo, px, nf * 2 * sizeof(double), hipMemcpyHostToDevice, s));
-            SVO_HIP(hipMemcpyAsync(b->d_bearing + 3 * fo, bearing, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
-            SVO_HIP(hipMemcpyAsync(b->d_point + 3 * fo, point, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
-            SVO_HIP(hipMemcpyAsync(b->d_has_point + fo, has_point, nf, hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_px + 2 * fo, px, nf * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_bearing + 3 * fo, bearing, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_point + 3 * fo, point, nf * 3 * sizeof(double), hipMemcpyHostToDevice, s));
+            SVO_HIP(stage_copy(c, b->d_has_point + fo, has_point, nf, hipMemcpyHostToDevice, s));
         }
-        SVO_HIP(hipMemcpyAsync(b->d_pairs + pair, &d, sizeof(d), hipMemcpyHostToDevice, s));
+        SVO_HIP(stage_copy(c, b->d_pairs + pair, &d, sizeof(d), hipMemcpyHostToDevice, s));
         SVO_HIP(hipStreamSynchronize(s));
     }
     b->pair_set[pair] = 1;
@@ -753,10 +790,25 @@ int svo_align_batch_results(svo_align_batch* b, double* poses, double* err, int3
     if (!b) return fail(SVO_ERR_ARG, "null argument");
     if (!b->ran) return fail(SVO_ERR_STATE, "batch has not been run");
     SVO_HIP(hipSetDevice(b->ctx->device));
-    hipStream_t s = b->ctx->stream;
-    if (poses) SVO_HIP(hipMemcpyAsync(poses, b->d_pose_out, (size_t)b->n_pairs * 7 * sizeof(double), hipMemcpyDeviceToHost, s));
-    if (err) SVO_HIP(hipMemcpyAsync(err, b->d_err, (size_t)b->n_pairs * sizeof(double), hipMemcpyDeviceToHost, s));
-    if (status) SVO_HIP(hipMemcpyAsync(status, b->d_status, (size_t)b->n_pairs * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    svo_ctx* c = b->ctx;
+    hipStream_t s = c->stream;
+    const size_t np = (size_t)b->n_pairs, bp = np * 7 * sizeof(double), be = np * sizeof(double), bs = np * sizeof(int32_t);
+    void* host = nullptr;
+    if (ctx_pinned(c, bp + be + bs, &host) == hipSuccess) {  // through the pinned block: kernel copies (stage_copy)
+        char* h = static_cast<char*>(host);
+        if (poses) SVO_HIP(stage_copy(c, h, b->d_pose_out, bp, hipMemcpyDeviceToHost, s));
+        if (err) SVO_HIP(stage_copy(c, h + bp, b->d_err, be, hipMemcpyDeviceToHost, s));
+        if (status) SVO_HIP(stage_copy(c, h + bp + be, b->d_status, bs, hipMemcpyDeviceToHost, s));
+        SVO_HIP(hipStreamSynchronize(s));
+        if (poses) std::memcpy(poses, h, bp);
+        if (err) std::memcpy(err, h + bp, be);
+        if (status) std::memcpy(status, h + bp + be, bs);
+        return SVO_OK;
+    }
+    (void)hipGetLastError();
+    if (poses) SVO_HIP(hipMemcpyAsync(poses, b->d_pose_out, bp, hipMemcpyDeviceToHost, s));
+    if (err) SVO_HIP(hipMemcpyAsync(err, b->d_err, be, hipMemcpyDeviceToHost, s));
+    if (status) SVO_HIP(hipMemcpyAsync(status, b->d_status, bs, hipMemcpyDeviceToHost, s));
     SVO_HIP(hipStreamSynchronize(s));
     return SVO_OK;
 }
@@ -841,7 +893,7 @@ static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_s
     double* d_px = d_rpx + 2 * nn;
     double* d_err = d_px + 2 * nn;
     int32_t* d_st = reinterpret_cast<int32_t*>(d_err + nn);
-    e = hipMemcpyAsync(base, hb, in_bytes, hipMemcpyHostToDevice, s);
+    e = stage_copy(c, base, hb, in_bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         svo::FeatureAlignArgs a;
         a.ref_grad = d_rg;
@@ -859,7 +911,7 @@ static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_s
         e = hipGetLastError();
     }
     if (e == hipSuccess)
-        e = hipMemcpyAsync(hb + out_off, static_cast<char*>(base) + out_off, total - out_off, hipMemcpyDeviceToHost, s);
+        e = stage_copy(c, hb + out_off, static_cast<char*>(base) + out_off, total - out_off, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_align: %s", hipGetErrorString(e));
     std::memcpy(px_inout, hb + out_off, nn * 2 * sizeof(double));
@@ -1067,7 +1119,7 @@ int svo_depth_update(svo_ctx* c, const svo_camera* cam, int32_t n_kf, const svo_
         std::memcpy(hb + o_kimg, kimg.data(), (size_t)n_kf * 8);
     }
     std::memcpy(hb + o_cpose, cur_pose, 56);
-    e = hipMemcpyAsync(db, hb, in_end, hipMemcpyHostToDevice, s);
+    e = stage_copy(c, db, hb, in_end, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         a.seeds = reinterpret_cast<svo_depth_seed*>(db + o_seeds);
         a.seeds_new = reinterpret_cast<svo_depth_seed*>(db + o_new);
@@ -1087,7 +1139,7 @@ int svo_depth_update(svo_ctx* c, const svo_camera* cam, int32_t n_kf, const svo_
         svo::launch_depth_update(a, s);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(hb + in_end, db + in_end, out_end - in_end, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = stage_copy(c, hb + in_end, db + in_end, out_end - in_end, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_depth_update: %s", hipGetErrorString(e));
     int32_t counts[2];
@@ -1141,13 +1193,13 @@ static int fs_detect(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_
     if (!staged) (void)hipGetLastError();
     int32_t cnt = 0;
     int32_t* h_n = staged ? static_cast<int32_t*>(host) : &cnt;
-    if (e == hipSuccess) e = hipMemcpyAsync(h_n, d_n, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = stage_copy(c, h_n, d_n, sizeof(int32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     cnt = *h_n;
     if (e == hipSuccess && cnt <= capacity && cnt > 0) {
         if (staged) {
             uint32_t* hk = reinterpret_cast<uint32_t*>(static_cast<char*>(host) + 64);
-            e = hipMemcpyAsync(hk, d_keys, (size_t)cnt * 4, hipMemcpyDeviceToHost, s);
+            e = stage_copy(c, hk, d_keys, (size_t)cnt * 4, hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e == hipSuccess) std::memcpy(keys, hk, (size_t)cnt * 4);
         } else {
@@ -1237,13 +1289,13 @@ int svo_feature_select_by_value(svo_ctx* c, const svo_pyramid_set* p, int32_t fr
         cell_px = pageable.data();
         h_occ = occupancy;
     }
-    e = hipMemcpyAsync(d_occ, h_occ, nc, hipMemcpyHostToDevice, s);
+    e = stage_copy(c, d_occ, h_occ, nc, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         const uint8_t* plane = p->d_base + (size_t)frame * p->stride + p->grad_off;
         svo::launch_feature_cell_max(plane, W, H, cell_size, gr, gc, d_occ, threshold, d_px, s);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(cell_px, d_px, (size_t)nc * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = stage_copy(c, cell_px, d_px, (size_t)nc * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_select_by_value: %s", hipGetErrorString(e));
     int32_t m = 0;
@@ -1335,9 +1387,9 @@ int svo_pose_optimize(svo_ctx* c, int32_t n_frames, const int32_t* feat_off, con
     for (const Piece& pc : in) {
         if (!pc.bytes) continue;
         if (staged) std::memcpy(hb + pc.off, pc.src, pc.bytes);
-        else if (e == hipSuccess) e = hipMemcpyAsync(db + pc.off, pc.src, pc.bytes, hipMemcpyHostToDevice, s);
+        else if (e == hipSuccess) e = stage_copy(c, db + pc.off, pc.src, pc.bytes, hipMemcpyHostToDevice, s);
     }
-    if (staged && e == hipSuccess) e = hipMemcpyAsync(db, hb, in_end, hipMemcpyHostToDevice, s);
+    if (staged && e == hipSuccess) e = stage_copy(c, db, hb, in_end, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         svo::PoseBAArgs a{reinterpret_cast<int32_t*>(db + o_off), reinterpret_cast<double*>(db + o_bear),
                           reinterpret_cast<double*>(db + o_pt), reinterpret_cast<uint8_t*>(db + o_has),
@@ -1351,10 +1403,10 @@ int svo_pose_optimize(svo_ctx* c, int32_t n_frames, const int32_t* feat_off, con
     struct Out { size_t off; void* dst; size_t bytes; };
     const Out out[] = {{o_pout, poses_inout, F * 56}, {o_err, err, F * 8}, {o_st, status, F * 4}, {o_vout, vis_inout, N}};
     if (staged) {
-        if (e == hipSuccess) e = hipMemcpyAsync(hb + in_end, db + in_end, out_end - in_end, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = stage_copy(c, hb + in_end, db + in_end, out_end - in_end, hipMemcpyDeviceToHost, s);
     } else {
         for (const Out& o : out)
-            if (o.bytes && e == hipSuccess) e = hipMemcpyAsync(o.dst, db + o.off, o.bytes, hipMemcpyDeviceToHost, s);
+            if (o.bytes && e == hipSuccess) e = stage_copy(c, o.dst, db + o.off, o.bytes, hipMemcpyDeviceToHost, s);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_pose_optimize: %s", hipGetErrorString(e));

@@ -43,6 +43,8 @@ if impl == svo_amd.SCALE_K2V:
     names = ("load", "classify", "barrier1", "publish+ranks", "sources", "barrier2", "targets", "exits", "scan",
              "crossing", "searches")
     print("K2V cycles per phase (thread 0, both passes): " + ", ".join(f"{a} {x:.0f}" for a, x in zip(names, out[12:23])))
+    log = out[24:152].reshape(-1, 2)
+    print("K2V block rounds (S, cycles; stamps build):", [tuple(int(x) for x in r) for r in log if r[0] >= 0])
     sys.exit(0)
 for p in range(2):
     cyc, nb, nl, hp = out[2 + 4 * p: 6 + 4 * p]
