@@ -57,12 +57,14 @@ constexpr int kScanGroup = 4;
 template <int R>
 struct VShared {
     static constexpr int kSteps = R * kVW;
-    double mb[kMbCap];                // mailbox; the one-wave segment (mb[0, 512)) and its mailbox (mb[512, 768))
+    // mailbox (mbx[0, kMbCap); the one-wave segment in [0, 512) and its mailbox in [512, 768)), then the
+    // per-lane dummy slots of the branch-free exchange (mbx[kMbCap + lane]): one array, so a lane's slot is
+    // one selected index
+    double mbx[kMbCap + 64];
     uint4 rec[kSteps];                // per step of the round: GE lo, GE hi, LE lo, LE hi
     uint32_t pre[kSteps];             // per step: #GE | #LE << 16 before it (each wave writes its own steps)
     double pub[6];                    // pre-values published by their owners (candidates 0-3, record 4)
     double bcd;                       // broadcast of the median between the passes
-    double dummy[64];                 // per-lane target of the branch-free stores of lanes with nothing to store
     double lrow[R - kVRegRows][kVT];  // rows 88..97 of the vector (the rest is in registers)
     uint32_t tmp[2 * kVW];            // per-wave counts of the prologue
 };
@@ -78,10 +80,19 @@ struct VDiag {  // svo_debug_robust_scale diagnostics
 };
 // a phase stamp of the debug kernel in the diagnostic build (make stamps: -DSVO_STAMPS, build/stamps/); in the
 // regular build the stamps are compiled out (they cost the debug kernel registers below the VGPR fence)
+#if defined(SVO_STAMPS_SMALL)  // (make stamps STAMPS_SMALL=1: the phases of block rounds of < 2048 positions only)
+constexpr bool kStampsSmall = true;
+#else
+constexpr bool kStampsSmall = false;
+#endif
 #if defined(SVO_STAMPS)
 #define VSTAMP(i) \
     do { \
-        if (dg && tid == 0) { const uint64_t t_ = clock64(); dg->ph[i] += t_ - tstamp; tstamp = t_; } \
+        if (dg && tid == 0) { \
+            const uint64_t t_ = clock64(); \
+            if (!kStampsSmall || small_round) dg->ph[i] += t_ - tstamp; \
+            tstamp = t_; \
+        } \
     } while (0)
 #else
 #define VSTAMP(i) \
@@ -295,6 +306,13 @@ __device__ __forceinline__ void vselx4(int r, const double (&x)[4], const uint64
           "v"((uint32_t)u2), "v"((uint32_t)(u2 >> 32)), "v"((uint32_t)u3), "v"((uint32_t)(u3 >> 32)),
           "s"(m[0]), "s"(m[1]), "s"(m[2]), "s"(m[3]), "s"(__builtin_amdgcn_readfirstlane(2 * r)));
 }
+// the lanes of m take a, the others b: one v_cndmask on the SGPR mask (the compiler's form of
+// ((m >> lane) & 1) ? a : b costs a 64-bit shift, an and and a compare per use)
+__device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
 // rows 0..87 of src (positions 512 r + tid) into the data VGPRs; lanes past `bytes` read 0 (buffer range)
 __device__ __forceinline__ void vload(const double* src, uint32_t bytes, int tid) {
     const uint64_t a = (uint64_t)src;
@@ -330,6 +348,7 @@ struct VSel {
     bool rec;
     double lo_val;
     int P;
+    bool small_round = false;  // (stamps build: the current block round has < 2048 positions)
 
     // ------------------------------------------------------------------ registers
     // body(r, x) for this wave's rows rlo..rhi, x the lane's value (kWrite: body may change it)
@@ -550,73 +569,92 @@ struct VSel {
         // this wave's step prefixes, lane j: row j (and row 64 + j): one LDS read each, then readlanes
         const uint32_t pre0 = sh.pre[((uint32_t)lane * kVW + (uint32_t)wave) % kSteps];
         const uint32_t pre1 = sh.pre[(((uint32_t)lane + 64u) * kVW + (uint32_t)wave) % kSteps];
-        double* const dl = sh.dummy + lane;
-        // the row's mailbox slots: the lanes of m ranked k0 < k <= k1 (okm) use mb[k - 1 - k0], the others
-        // their dummy slot.  Branch-free: the range test is one unsigned compare, okm its ballot and m.
+        // a lane's mailbox index: ranks k0 < k <= k1 of m (okm) use mbx[k - 1 - k0], the other lanes their
+        // dummy slot mbx[kMbCap + lane].  kk = k - 1 - k0 is one mbcnt over a scalar base (side 0: ranks from
+        // the left, pp's GE count + the GE lanes below + 1; side 1: ranks from the right, totL - (pp's LE
+        // count + the LE lanes below)); the range test is one unsigned compare, the slot one v_cndmask on
+        // the SGPR mask
         const uint32_t nk = k1 - k0;
-        auto slot = [&](int r, uint64_t m, uint64_t& okm) __attribute__((always_inline)) -> double* {
-            const uint32_t pp = uni(lane_read(r < 64 ? pre0 : pre1, r & 63));
-            const uint32_t k = side == 0 ? (pp & 0xFFFFu) + lanes_below(m) + 1u : totL - ((pp >> 16) + lanes_below(m));
-            const uint32_t kk = k - 1u - k0;
+        const uint32_t dslot = kMbCap + (uint32_t)lane;
+        // the scalar part of kk for the step prefix pp (an opaque copy: the compiler would otherwise fold the
+        // side-1 base back into the per-lane arithmetic)
+        auto kbase = [&](uint32_t pp) __attribute__((always_inline)) -> uint32_t {
+            uint32_t b = side == 0 ? (pp & 0xFFFFu) - k0 : totL - 1u - k0 - (pp >> 16);
+            asm volatile("" : "+s"(b));
+            return b;
+        };
+        auto slot_pp = [&](uint32_t pp, uint64_t m, uint64_t& okm) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t b = kbase(pp);
+            const uint32_t kk = side == 0 ? __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, b))
+                                          : b - lanes_below(m);
             okm = m & __ballot(kk < nk);
-            return ((okm >> lane) & 1ull) ? sh.mb + kk : dl;
+            return lane_sel(okm, kk, dslot);
+        };
+        auto slot = [&](int r, uint64_t m, uint64_t& okm) __attribute__((always_inline)) -> uint32_t {
+            return slot_pp(r < 64 ? lane_read(pre0, r) : lane_read(pre1, r - 64), m, okm);
         };
         auto mask = [&](int r, double x, bool reg) __attribute__((always_inline)) -> uint64_t {
             if (chunked) return rec_mask((uint32_t)(r * kVW + wave), side);
             if (side == 0) return (reg ? vcmp_ge(r, p) : __ballot(!(x < p))) & w.ge(r);
             return (reg ? vcmp_le(r, p) : __ballot(!(p < x))) & w.le(r);
         };
+        double* const mbx = sh.mbx;
         // register rows, four per iteration (independent chains: their compares, ranks and LDS accesses
-        // overlap), then the rest one at a time
+        // overlap), then the rest one at a time; rows below 64 take their prefixes from pre0, the others from
+        // pre1 (two loops: one readlane per row, no select)
         const int r1 = w.rhi < kVRegRows - 1 ? w.rhi : kVRegRows - 1;
-        int r = w.rlo;
-        for (; r + 3 <= r1; r += 4) {
-            uint64_t m[4];
-            if (chunked) {
+        auto reg_rows = [&](int ra, int rb, uint32_t prex, int roff) __attribute__((always_inline)) {
+            int r = ra;
+            for (; r + 3 <= rb; r += 4) {
+                uint64_t m[4];
+                if (chunked) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) m[j] = rec_mask((uint32_t)((r + j) * kVW + wave), side);
-            } else {
-                if (side == 0) vcmpx4<0>(r, p, m);
-                else vcmpx4<1>(r, p, m);
+                    for (int j = 0; j < 4; ++j) m[j] = rec_mask((uint32_t)((r + j) * kVW + wave), side);
+                } else {
+                    if (side == 0) vcmpx4<0>(r, p, m);
+                    else vcmpx4<1>(r, p, m);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) m[j] &= side == 0 ? w.ge(r + j) : w.le(r + j);
+                    for (int j = 0; j < 4; ++j) m[j] &= side == 0 ? w.ge(r + j) : w.le(r + j);
+                }
+                uint64_t okm[4];
+                uint32_t a[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a[j] = slot_pp(lane_read(prex, r + j - roff), m[j], okm[j]);
+                if (kWrite) {
+                    double x[4];
+                    vgetx4(r, x);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) mbx[a[j]] = x[j];
+                } else {
+                    double t[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) t[j] = mbx[a[j]];
+                    vselx4(r, t, okm);
+                }
             }
-            uint64_t okm[4];
-            double* a[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] = slot(r + j, m[j], okm[j]);
-            if (kWrite) {
-                double x[4];
-                vgetx4(r, x);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) *a[j] = x[j];
-            } else {
-                double t[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) t[j] = *a[j];
-                vselx4(r, t, okm);
+            for (; r <= rb; ++r) {
+                uint64_t okm;
+                const uint32_t a0 = slot_pp(lane_read(prex, r - roff), mask(r, 0.0, true), okm);
+                if (kWrite) {
+                    mbx[a0] = vget(r);
+                } else {
+                    const double t0 = mbx[a0];
+                    vsel(r, t0, okm);
+                }
             }
-        }
-        for (; r <= r1; ++r) {
-            uint64_t okm;
-            double* const a0 = slot(r, mask(r, 0.0, true), okm);
-            if (kWrite) {
-                *a0 = vget(r);
-            } else {
-                const double t0 = *a0;
-                vsel(r, t0, okm);
-            }
-        }
+        };
+        reg_rows(w.rlo, r1 < 63 ? r1 : 63, pre0, 0);
+        reg_rows(w.rlo > 64 ? w.rlo : 64, r1, pre1, 64);
         // LDS rows
         for (int r = w.rlo > kVRegRows ? w.rlo : kVRegRows; r <= w.rhi; ++r) {
             double& y = sh.lrow[r - kVRegRows][tid];
             const double x = y;
             uint64_t okm;
-            double* const a = slot(r, mask(r, x, false), okm);
+            const uint32_t a = slot(r, mask(r, x, false), okm);
             if (kWrite) {
-                *a = x;
+                mbx[a] = x;
             } else {
-                const double t = *a;
+                const double t = mbx[a];
                 y = ((okm >> lane) & 1ull) ? t : x;
             }
         }
@@ -637,6 +675,7 @@ struct VSel {
 #if defined(SVO_STAMPS)
         const uint64_t tround = tstamp;
         const uint32_t S0 = l - f;
+        small_round = S0 < 2048;
 #endif
         classify(p, ch, x0);
         VSTAMP(1);
@@ -722,7 +761,7 @@ struct VSel {
                 if (need) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
-                        if (ck[i] > k0 && ck[i] <= k1) cand[i] = uni(sh.mb[ck[i] - 1u - k0]);
+                        if (ck[i] > k0 && ck[i] <= k1) cand[i] = uni(sh.mbx[ck[i] - 1u - k0]);
                 }
             }
             if (it + 1 < nch) __syncthreads();
@@ -877,13 +916,13 @@ struct VSel {
             }
             if (dg && tid == 0) dg->heap[P] = 1;
         } else {
-            double* const seg = sh.mb;  // positions f0 + i
+            double* const seg = sh.mbx;  // positions f0 + i
             const uint32_t f0 = f;
-            dump(seg, f0, sh.dummy);
+            dump(seg, f0, sh.mbx + kMbCap);
             __syncthreads();
             if (wave == 0) {
                 uint32_t nw = 0;
-                wave_rounds(seg, sh.mb + kOneWave, nw);
+                wave_rounds(seg, sh.mbx + kOneWave, nw);
                 if (tid == 0) {
                     if (l - f <= 3) {  // std::__insertion_sort of the last <= 3
                         const uint32_t n = l - f;
@@ -1008,6 +1047,7 @@ debug_robust_scale_v_kernel(const double* v, uint32_t M, uint32_t n, double* gse
         }
         for (int i = 0; i < 12; ++i) out[12 + i] = (double)dg.ph[i];
         for (int i = 0; i < 128; ++i) out[24 + i] = i / 2 < (int)dg.nlog ? (double)dg.log[i / 2][i % 2] : -1.0;
+
     }
 }
 

@@ -6,6 +6,7 @@ oracle (pose <= 1e-9, status exact) and repeat its own single-pair run bit for b
 svo_align_batch_set_pairs path must give the identical batch.  Both median modes."""
 import numpy as np
 import pytest
+import torch  # noqa: F401  (before libsvo_hip initialises HIP: torch's own HIP runtime then finds the GPU too)
 
 import svo_amd
 import svo_amd.synth as synth
@@ -94,7 +95,6 @@ def test_gpu_two_chain_batch(mode):
             hi = min(P, lo + split)
             args = packed(sc, range(lo, hi))
             if on_dev:
-                import torch
                 feats = [torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0") for a in args[3:]]
                 torch.cuda.synchronize()
                 args = (*args[:3], *feats)
