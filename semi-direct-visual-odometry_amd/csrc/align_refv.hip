@@ -375,12 +375,17 @@ struct VSel {
         if (r < kVRegRows) vset(r, x);
         else sh.lrow[r - kVRegRows][tid] = x;
     }
-    __device__ __forceinline__ void load(const double* src, bool mad, double med) {
+    // this thread's rows of src: registers and LDS rows
+    __device__ __forceinline__ void load_raw(const double* src) {
         vload(src, M * 8u, tid);  // (rows past M hold 0: never inside a segment)
         for (int r = kVRegRows; r < R; ++r) {
             const uint32_t q = (uint32_t)r * kVT + (uint32_t)tid;
             sh.lrow[r - kVRegRows][tid] = q < M ? src[q] : 0.0;
         }
+    }
+    // preloaded: the rows were loaded already (the MAD pass's rows, during the median pass's one-wave rounds)
+    __device__ __forceinline__ void load(const double* src, bool mad, double med, bool preloaded) {
+        if (!preloaded) load_raw(src);
         if (mad) {  // src/algorithm.cpp:860-863 (DBL_MAX stays DBL_MAX)
             rows<true>(0, R - 1, [&](int, double& x) __attribute__((always_inline)) { x = fabs(x - med); });
         }
@@ -875,10 +880,14 @@ struct VSel {
 
     // ------------------------------------------------------------------ std::nth_element(vec, vec + nth)
     // (vec[nth - 1], vec[nth]) of the post-state, on thread 0
-    __device__ __forceinline__ void select(const double* src, bool mad, double med, double& hi, double& lo) {
+    // preload_next: load the raw rows for the MAD pass while wave 0 runs this pass's one-wave rounds (the other
+    // waves' registers are free after the dump); returns through `preloaded` whether it did
+    __device__ __forceinline__ void select(const double* src, bool mad, double med, bool preloaded, bool preload_next,
+                                           double& hi, double& lo, bool& did_preload) {
         const uint64_t t0 = dg ? clock64() : 0;
         uint64_t tstamp = t0;
-        load(src, mad, med);
+        did_preload = false;
+        load(src, mad, med, preloaded);
         VSTAMP(0);
         f = 0;
         l = M;
@@ -920,6 +929,8 @@ struct VSel {
             const uint32_t f0 = f;
             dump(seg, f0, sh.mbx + kMbCap);
             __syncthreads();
+            did_preload = preload_next;
+            if (preload_next && wave != 0) load_raw(src);
             if (wave == 0) {
                 uint32_t nw = 0;
                 wave_rounds(seg, sh.mbx + kOneWave, nw);
@@ -939,6 +950,7 @@ struct VSel {
                     }
                     if (dg) dg->nwave[P] = nw;
                 }
+                if (preload_next) load_raw(src);  // (after the rounds: they used only LDS)
             }
         }
         __syncthreads();  // seg / mailbox / gseg are reused by the next pass
@@ -963,10 +975,13 @@ __device__ __forceinline__ void refv_robust_scale(const double* src, VShared<R>&
     s.wave = (int)uni((uint32_t)(s.tid >> 6));
     const bool even = (M & 1u) == 0 && s.nth >= 1;  // mid == 0 (UB in the reference) reads vec[mid]
     double m0 = 0.0;
+    bool pre = false;
     for (int P = 0; P < 2; ++P) {  // one copy of the selection for both passes
         s.P = P;
         double lo = 0.0, hi = 0.0;
-        s.select(src, P == 1, m0, hi, lo);
+        bool did = false;
+        s.select(src, P == 1, m0, pre, P == 0, hi, lo, did);
+        pre = did;
         if (s.tid == 0) sh.bcd = even ? (lo + hi) / 2.0 : hi;
         __syncthreads();
         const double r = uni(sh.bcd);
