@@ -786,26 +786,35 @@ struct VSel {
     }
 
     // ------------------------------------------------------------------ rounds of <= 512 positions (wave 0)
-    // No barriers: the segment stays in LDS (seg[i] = position f0 + i), lane L of step j reads position
-    // f0 + 64 j + L each round; the candidates are broadcast reads, the masks compares, the counts / crossing
-    // / rank searches scalars, the swaps go through a mailbox (a wave's LDS accesses complete in program
-    // order).  Stops at <= 3 positions or depth 0.
+    // No barriers: wave 0 takes the segment (seg[i] = position f0 + i, from the dump) into its data rows 0..7
+    // (position f0 + 64 j + L in lane L of row j; the rows' own values are dead after the dump), so a round
+    // reads no segment memory: the candidates are readlanes, the masks compares, the counts / crossing / rank
+    // searches scalars and ballots, the swaps go through the mailbox mb (a wave's LDS accesses complete in
+    // program order) into the rows by masked selects.  Stops at <= 3 positions or depth 0; then the rows go
+    // back to seg for the final sort or the heap select.
+    __device__ __forceinline__ double cand_at(uint32_t q) const {
+        return uni(lane_read(vget((int)(q >> 6)), (int)(q & 63u)));
+    }
     __device__ __forceinline__ void wave_rounds(double* seg, double* mb, uint32_t& nrounds) {
         const uint32_t f0 = f, me = (uint32_t)lane;
         uint32_t fr = 0, lr = l - f;
         const uint32_t nrel = nth - f0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vset(j, seg[64 * j + lane]);
+        // the mailbox and each lane's dummy slot as indices into sh.mbx
+        const uint32_t mb0 = (uint32_t)(mb - sh.mbx), dslot = kMbCap + me;
+        double* const mbx = sh.mbx;
         while (lr - fr > 3 && depth > 0) {
             --depth;
             ++nrounds;
             const uint32_t A = fr + 1, B = fr + (lr - fr) / 2, C = lr - 1;
-            const double a = uni(seg[A]), b = uni(seg[B]), c = uni(seg[C]), xv = uni(seg[fr]);
+            const double a = cand_at(A), b = cand_at(B), c = cand_at(C), xv = cand_at(fr);
             uint32_t chh;
             double pe;
             median3(a, b, c, A, B, C, chh, pe);
-            if (me == 0) {  // std::iter_swap(first, chosen)
-                seg[fr] = pe;
-                seg[chh] = xv;
-            }
+            // std::iter_swap(first, chosen)
+            vsel((int)(fr >> 6), pe, 1ull << (fr & 63u));
+            vsel((int)(chh >> 6), xv, 1ull << (chh & 63u));
             const uint32_t js = fr >> 6, je = (lr - 1) >> 6;
             double w[8];
             uint64_t ge[8], le[8];
@@ -816,8 +825,8 @@ struct VSel {
                 ge[j] = le[j] = 0;
                 w[j] = 0.0;
                 if ((uint32_t)j >= js && (uint32_t)j <= je) {
-                    const uint32_t base = 64u * (uint32_t)j, i = base + me;
-                    w[j] = seg[i < lr ? i : fr];
+                    const uint32_t base = 64u * (uint32_t)j;
+                    w[j] = vget(j);
                     const uint32_t lo = fr > base ? (fr - base < 64u ? fr - base : 64u) : 0u;
                     const uint32_t hi = lr > base ? (lr - base < 64u ? lr - base : 64u) : 0u;
                     const uint64_t inm = low_mask(hi) & ~low_mask(lo);
@@ -836,7 +845,7 @@ struct VSel {
 #pragma unroll
             for (int j = 0; j < 8; ++j)
                 if ((uint32_t)j >= js && (uint32_t)j <= je && gp[j] < tL - lp[j]) { gcar = gp[j]; lcar = tL - lp[j]; a0 = ge[j]; b0m = le[j]; }
-            const uint32_t ks = crossing_ks(gcar, lcar, a0, b0m);
+            const uint32_t ks = uni(wave_crossing_ks(gcar, lcar, a0, b0m));
             auto rank_pos = [&](int kind, uint32_t rank) -> uint32_t {  // the last step starting below the rank
                 if (rank == 0 || rank > (kind ? tL : tG)) return kNone;
                 uint32_t pre = 0, jj = 0;
@@ -846,34 +855,39 @@ struct VSel {
                     const uint32_t pj = kind ? lp[j] : gp[j];
                     if ((uint32_t)j >= js && (uint32_t)j <= je && pj < rank) { pre = pj; jj = (uint32_t)j; mk = kind ? le[j] : ge[j]; }
                 }
-                return 64u * jj + select_bit(mk, rank - pre - 1u);
+                return 64u * jj + wave_select_bit(mk, rank - pre - 1u);
             };
             const uint32_t lk1 = rank_pos(0, ks + 1), rk = ks >= 1 ? rank_pos(1, tL - ks + 1) : kNone;
             const uint32_t cut = lk1 < rk ? lk1 : rk;
             const bool right = cut <= nrel;
             if (cut == nrel && !rec && nrel >= 1) {
                 const uint32_t lk = ks >= 1 ? rank_pos(0, ks) : kNone;
-                lo_val = uni(seg[lk == cut - 1 ? rk : cut - 1]);
+                lo_val = cand_at(lk == cut - 1 ? rk : cut - 1);  // (pre-values: the swaps come below)
                 rec = true;
             }
-            // sources to the mailbox, then the kept side's targets take it (straight into seg)
+            // sources to the mailbox, then the kept side's targets take it (masked selects into the rows)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if ((uint32_t)j < js || (uint32_t)j > je) continue;
                 const uint64_t m = right ? ge[j] : le[j];
                 const uint32_t k = right ? gp[j] + lanes_below(m) + 1u : tL - (lp[j] + lanes_below(m));
-                if (((m >> me) & 1ull) && k <= ks) mb[k - 1] = w[j];
+                const uint64_t okm = m & __ballot(k <= ks);
+                mbx[lane_sel(okm, mb0 + k - 1u, dslot)] = w[j];
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 if ((uint32_t)j < js || (uint32_t)j > je) continue;
                 const uint64_t m = right ? le[j] : ge[j];
                 const uint32_t k = right ? tL - (lp[j] + lanes_below(m)) : gp[j] + lanes_below(m) + 1u;
-                if (((m >> me) & 1ull) && k <= ks) seg[64u * (uint32_t)j + me] = mb[k - 1];
+                const uint64_t okm = m & __ballot(k <= ks);
+                const double t = mbx[lane_sel(okm, mb0 + k - 1u, dslot)];
+                vsel(j, t, okm);
             }
             if (right) fr = cut;
             else lr = cut;
         }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) seg[64 * j + lane] = vget(j);
         f = f0 + fr;
         l = f0 + lr;
     }
