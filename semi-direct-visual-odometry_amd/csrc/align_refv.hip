@@ -512,10 +512,16 @@ struct VSel {
     }
     // the packed prefix of a block-uniform entry
     __device__ __forceinline__ uint32_t pk_at(const Scan& S, uint32_t e) const {
-        const uint32_t li = e / S.K, ii = e - li * S.K;
-        uint32_t x = S.pk[0];
+        const uint32_t li = uni(e / S.K), ii = uni(e - li * S.K);
+        // an and-or chain in asm (one v_and_or_b32 per slot): written as plain selects, the compiler turned it
+        // into an indexed load and kept pk[] in scratch memory (a store per entry every scan, a memory round
+        // trip per lookup)
+        uint32_t x = 0;
 #pragma unroll
-        for (int i = 1; i < kKl; ++i) x = ii == (uint32_t)i ? S.pk[i] : x;
+        for (int i = 0; i < kKl; ++i) {
+            const uint32_t msk = ii == (uint32_t)i ? ~0u : 0u;
+            asm volatile("v_and_or_b32 %0, %1, %2, %3" : "=v"(x) : "v"(S.pk[i]), "s"(msk), "v"(x));
+        }
         return uni(lane_read(x, (int)li));
     }
     __device__ __forceinline__ uint64_t rec_mask(uint32_t s, int kind) const {
