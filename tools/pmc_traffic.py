@@ -26,7 +26,8 @@ def per_kernel(pass_dir, counter):
             if "svo::align" not in name or r["Counter_Name"] != counter:
                 continue
             tot[name.split("(")[0]] += float(r["Counter_Value"]) * 1024.0
-            if "align_scale_kernel" in name or "align_scale_ref_kernel" in name:  # K2 / K2R: once per level and chain
+            if any(k in name for k in ("align_scale_kernel", "align_scale_ref_kernel", "align_scale_refv_kernel")):
+                # K2 / K2R / K2V: once per level and chain
                 runs += 1
     return tot, runs
 
@@ -54,7 +55,7 @@ def main():
         "per_kernel_bytes_per_launch": {k: {kk: round(vv) for kk, vv in v.items()} for k, v in per.items()},
         "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes",
         "calibration_note": "MI355X_MICROARCH.md calibrates the FETCH_SIZE x2 only for 16-B/lane coalesced streams; "
-                            "the 8-B/lane gathers of K1/K2R are uncalibrated, so the read bytes are an estimate",
+                            "the 8-B/lane accesses of K1 / K2V (and K2R) are uncalibrated, so the read bytes are an estimate",
     }, indent=1))
 
 
