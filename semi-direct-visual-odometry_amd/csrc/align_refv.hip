@@ -310,7 +310,7 @@ __device__ __forceinline__ void vselx4(int r, const double (&x)[4], const uint64
 // ((m >> lane) & 1) ? a : b costs a 64-bit shift, an and and a compare per use)
 __device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b) {
     uint32_t r;
-    asm volatile("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
     return r;
 }
 // rows 0..87 of src (positions 512 r + tid) into the data VGPRs; lanes past `bytes` read 0 (buffer range)
@@ -520,7 +520,7 @@ struct VSel {
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
             const uint32_t msk = ii == (uint32_t)i ? ~0u : 0u;
-            asm volatile("v_and_or_b32 %0, %1, %2, %3" : "=v"(x) : "v"(S.pk[i]), "s"(msk), "v"(x));
+            asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(x) : "v"(S.pk[i]), "s"(msk), "v"(x));
         }
         return uni(lane_read(x, (int)li));
     }

@@ -734,11 +734,16 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         static const int env_stagger = getenv("SVO_STAGGER") ? atoi(getenv("SVO_STAGGER")) : -1;  //  read once)
         const int ns = env_chains ? std::max(2, std::min(4, env_chains)) : kSplits;
         const int32_t per = (b->n_pairs / ns + 7) / 8 * 8;
-        // Reference semantics: chain 1 starts when chain 0's first K1 is done (launch mark 2), so that each
-        // chain's K1 / K3 run under the other chain's K2R instead of both chains meeting in K1 / K3 at every
+        // Reference semantics with K2R: chain 1 starts when chain 0's first K1 is done (launch mark 2), so that
+        // each chain's K1 / K3 run under the other chain's K2R instead of both chains meeting in K1 / K3 at every
         // level (MI355X, 512 pairs: 88.4k vs 78.4k pairs/s; marks 3 / 4 / 7: 79k / 74k / 67k).  The exact mode
         // runs unstaggered (round 1: staggering by 1-3 kernels cost 1-6 %).  SVO_STAGGER=k overrides.
-        const int stagger = env_stagger >= 0 ? env_stagger : (b->params.median_mode == SVO_MEDIAN_REFERENCE ? 2 : 0);
+        // K2V (the default reference-mode kernel whenever the vector fits its registers) fills whole CUs, so
+        // the other chain's K1 / K3 run only between its launches whatever the stagger: unstaggered measured
+        // best (MI355X, 512 pairs: stagger 0 / 1 / 2 / 3 = 119.1k / 118.4k / 117.3k / 117.4k pairs/s).
+        const bool k2v = svo::scale_impl() != SVO_SCALE_K2R && (int64_t)b->max_f * b->area <= svo::refv_max_slots();
+        const int stagger = env_stagger >= 0 ? env_stagger
+                                             : (b->params.median_mode == SVO_MEDIAN_REFERENCE && !k2v ? 2 : 0);
         if (stagger < 0 || stagger > 1 + 3 * (b->params.max_level - b->params.min_level + 1))
             return fail(SVO_ERR_ARG, "SVO_STAGGER=%d outside the chain's launch marks", stagger);
         SVO_HIP(hipEventRecord(c->fork, c->stream));
