@@ -81,9 +81,9 @@ struct VDiag {  // svo_debug_robust_scale diagnostics
 // a phase stamp of the debug kernel in the diagnostic build (make stamps: -DSVO_STAMPS, build/stamps/); in the
 // regular build the stamps are compiled out (they cost the debug kernel registers below the VGPR fence)
 #if defined(SVO_STAMPS_SMALL)  // (make stamps STAMPS_SMALL=1: the phases of block rounds of < 2048 positions only)
-constexpr bool kStampsSmall = true;
+[[maybe_unused]] constexpr bool kStampsSmall = true;
 #else
-constexpr bool kStampsSmall = false;
+[[maybe_unused]] constexpr bool kStampsSmall = false;
 #endif
 #if defined(SVO_STAMPS)
 #define VSTAMP(i) \

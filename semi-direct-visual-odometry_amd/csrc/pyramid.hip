@@ -28,7 +28,10 @@ __device__ __forceinline__ int reflect101(int i, int n) {
 // 8-row x 256-column destination tile: vertical [1 4 6 4 1] pass first, one thread per source column
 // reading its 20 source rows straight from global memory (consecutive threads, consecutive bytes),
 // 16-bit column sums into LDS, then the horizontal pass from LDS.
-constexpr int kDnW = 256, kDnH = 8;
+#ifndef SVO_DNH
+#define SVO_DNH 8
+#endif
+constexpr int kDnW = 256, kDnH = SVO_DNH;
 constexpr int kDnCols = 2 * kDnW + 4, kDnRows = 2 * kDnH + 4;
 
 __global__ void __launch_bounds__(256) pyr_down_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
