@@ -445,14 +445,29 @@ struct VSel {
         if (((f >> 6) & (kVW - 1)) == (uint32_t)wave) row_set((int)(f >> 9), f & 63u, p);
         if (((ch >> 6) & (kVW - 1)) == (uint32_t)wave) row_set((int)(ch >> 9), ch & 63u, x0);
         const WaveRows w = wave_segment(f >> 6, (l - 1) >> 6);
+        if (w.rlo > w.rhi) return;
         uint4* const recw = sh.rec + wave;
         auto put = [&](int r, uint64_t ge, uint64_t le) __attribute__((always_inline)) {
-            ge &= w.ge(r);
-            le &= w.le(r);
             if (lane == 0) recw[r * kVW] = make_uint4((uint32_t)ge, (uint32_t)(ge >> 32), (uint32_t)le, (uint32_t)(le >> 32));
         };
-        const int r1 = w.rhi < kVRegRows - 1 ? w.rhi : kVRegRows - 1;
-        int r = w.rlo;
+        // the wave's first and last rows can be partial (the first also drops position f from GE): masked
+        // one at a time; the rows between take the full compare masks with no scalar mask arithmetic
+        auto edge = [&](int r, uint64_t gm, uint64_t lm) __attribute__((always_inline)) {
+            uint64_t ge, le;
+            if (r < kVRegRows) {
+                vcmp2(r, p, ge, le);
+            } else {
+                const double x = sh.lrow[r - kVRegRows][tid];
+                ge = __ballot(!(x < p));
+                le = __ballot(!(p < x));
+            }
+            put(r, ge & gm, le & lm);
+        };
+        edge(w.rlo, w.ge_first, w.le_first);
+        if (w.rhi > w.rlo) edge(w.rhi, w.last, w.last);
+        const int ra = w.rlo + 1, rb = w.rhi - 1;  // interior rows
+        const int r1 = rb < kVRegRows - 1 ? rb : kVRegRows - 1;
+        int r = ra;
         for (; r + 3 <= r1; r += 4) {
             uint64_t ge[4], le[4];
             vcmp2x4(r, p, ge, le);
@@ -464,7 +479,7 @@ struct VSel {
             vcmp2(r, p, ge, le);
             put(r, ge, le);
         }
-        for (int r = w.rlo > kVRegRows ? w.rlo : kVRegRows; r <= w.rhi; ++r) {
+        for (int r = ra > kVRegRows ? ra : kVRegRows; r <= rb; ++r) {
             const double x = sh.lrow[r - kVRegRows][tid];
             put(r, __ballot(!(x < p)), __ballot(!(p < x)));
         }
@@ -604,16 +619,17 @@ struct VSel {
         auto slot = [&](int r, uint64_t m, uint64_t& okm) __attribute__((always_inline)) -> uint32_t {
             return slot_pp(r < 64 ? lane_read(pre0, r) : lane_read(pre1, r - 64), m, okm);
         };
+        // the side's mask of row r (register row, or the LDS row value x); the records when chunked (masked
+        // at the classification); interior rows need no range mask (the edge rows are peeled below)
         auto mask = [&](int r, double x, bool reg) __attribute__((always_inline)) -> uint64_t {
             if (chunked) return rec_mask((uint32_t)(r * kVW + wave), side);
-            if (side == 0) return (reg ? vcmp_ge(r, p) : __ballot(!(x < p))) & w.ge(r);
-            return (reg ? vcmp_le(r, p) : __ballot(!(p < x))) & w.le(r);
+            if (side == 0) return reg ? vcmp_ge(r, p) : __ballot(!(x < p));
+            return reg ? vcmp_le(r, p) : __ballot(!(p < x));
         };
         double* const mbx = sh.mbx;
         // register rows, four per iteration (independent chains: their compares, ranks and LDS accesses
         // overlap), then the rest one at a time; rows below 64 take their prefixes from pre0, the others from
         // pre1 (two loops: one readlane per row, no select)
-        const int r1 = w.rhi < kVRegRows - 1 ? w.rhi : kVRegRows - 1;
         auto reg_rows = [&](int ra, int rb, uint32_t prex, int roff) __attribute__((always_inline)) {
             int r = ra;
             for (; r + 3 <= rb; r += 4) {
@@ -624,8 +640,6 @@ struct VSel {
                 } else {
                     if (side == 0) vcmpx4<0>(r, p, m);
                     else vcmpx4<1>(r, p, m);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) m[j] &= side == 0 ? w.ge(r + j) : w.le(r + j);
                 }
                 uint64_t okm[4];
                 uint32_t a[4];
@@ -654,21 +668,37 @@ struct VSel {
                 }
             }
         };
-        reg_rows(w.rlo, r1 < 63 ? r1 : 63, pre0, 0);
-        reg_rows(w.rlo > 64 ? w.rlo : 64, r1, pre1, 64);
-        // LDS rows
-        for (int r = w.rlo > kVRegRows ? w.rlo : kVRegRows; r <= w.rhi; ++r) {
-            double& y = sh.lrow[r - kVRegRows][tid];
-            const double x = y;
+        // one row with an explicit range mask gm (register or LDS row)
+        auto one_row = [&](int r, uint64_t gm) __attribute__((always_inline)) {
             uint64_t okm;
-            const uint32_t a = slot(r, mask(r, x, false), okm);
-            if (kWrite) {
-                mbx[a] = x;
+            if (r < kVRegRows) {
+                const uint32_t a0 = slot(r, mask(r, 0.0, true) & gm, okm);
+                if (kWrite) {
+                    mbx[a0] = vget(r);
+                } else {
+                    const double t0 = mbx[a0];
+                    vsel(r, t0, okm);
+                }
             } else {
-                const double t = mbx[a];
-                y = ((okm >> lane) & 1ull) ? t : x;
+                double& y = sh.lrow[r - kVRegRows][tid];
+                const double x = y;
+                const uint32_t a = slot(r, mask(r, x, false) & gm, okm);
+                if (kWrite) {
+                    mbx[a] = x;
+                } else {
+                    const double t = mbx[a];
+                    y = ((okm >> lane) & 1ull) ? t : x;
+                }
             }
-        }
+        };
+        // edge rows (partial: masked), then the interior rows (full masks)
+        one_row(w.rlo, side == 0 ? w.ge_first : w.le_first);
+        if (w.rhi > w.rlo) one_row(w.rhi, w.last);
+        const int ra = w.rlo + 1, rb = w.rhi - 1;
+        const int r1i = rb < kVRegRows - 1 ? rb : kVRegRows - 1;
+        reg_rows(ra, r1i < 63 ? r1i : 63, pre0, 0);
+        reg_rows(ra > 64 ? ra : 64, r1i, pre1, 64);
+        for (int r = ra > kVRegRows ? ra : kVRegRows; r <= rb; ++r) one_row(r, ~0ull);
     }
 
     // ------------------------------------------------------------------ one block round
