@@ -357,6 +357,24 @@ def latency_lines(ctx, scenes, camera, cam, patch, L, nf, mode, reps=20):
         if r >= 3:
             ts.append(time.perf_counter() - t)
     out["n_pairs_1_class_surface_ms"] = round(float(np.median(ts)) * 1e3, 4)
+    # the same per-frame call through the C++ mirror (host/svo.hpp ImageAlignment via build/svo_host_check
+    # align ... REPS): what the reference's C++ System pays, without the Python mirror's gather of the
+    # Feature objects; reported only when its pose equals the class surface's bit for bit
+    py_pose = np.array(cur.abs_pose, dtype=np.float64)
+    out["n_pairs_1_cpp_mirror_ms"] = None
+    exe = os.path.join(ROOT, "semi-direct-visual-odometry_amd", "build", "svo_host_check")
+    if os.path.exists(exe):
+        import subprocess
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            paths = synth.write_align_problem(s, td)
+            r = subprocess.run([exe, "align", *paths, str(patch), "0", str(L - 1), str(int(mode)), str(reps)],
+                               capture_output=True, text=True, timeout=120)
+            lines = r.stdout.splitlines() if r.returncode == 0 else []
+            if len(lines) == 3 and lines[2].startswith("ms "):
+                cpp_pose = np.array([float(x) for x in lines[0].split()[2:9]])
+                if np.array_equal(cpp_pose, py_pose):
+                    out["n_pairs_1_cpp_mirror_ms"] = round(float(lines[2].split()[1]), 4)
     for n in (64, 512):
         D = len(scenes)
         ps = svo_amd.PyramidSet(3 * n, cam["width"], cam["height"], L, ctx)

@@ -277,18 +277,17 @@ class Frame:
 
 
 def _feature_arrays(frames):
+    """The frames' features as SoA arrays (px, bearing, point, has_point), in frame then feature order."""
     feats = [f for fr in frames for f in fr.features]
     n = len(feats)
-    px = np.zeros((max(n, 1), 2))
-    br = np.zeros((max(n, 1), 3))
-    pt = np.zeros((max(n, 1), 3))
-    hp = np.zeros(max(n, 1), np.uint8)
-    for i, f in enumerate(feats):
-        px[i] = f.pixel_position
-        br[i] = f.bearing_vec
-        if f.point is not None:
-            pt[i] = f.point.position
-            hp[i] = 1
+    if n == 0:
+        return np.zeros((1, 2)), np.zeros((1, 3)), np.zeros((1, 3)), np.zeros(1, np.uint8)
+    px = np.array([f.pixel_position for f in feats], dtype=np.float64).reshape(n, 2)
+    br = np.array([f.bearing_vec for f in feats], dtype=np.float64).reshape(n, 3)
+    pts = [f.point for f in feats]
+    hp = np.fromiter((p is not None for p in pts), dtype=np.uint8, count=n)
+    z = np.zeros(3)
+    pt = np.array([z if p is None else p.position for p in pts], dtype=np.float64).reshape(n, 3)
     return px, br, pt, hp
 
 

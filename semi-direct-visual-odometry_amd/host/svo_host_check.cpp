@@ -23,6 +23,7 @@
 //                                  cur pose (the second call reuses the object's batch); DATA.bin (doubles):
 //                                  fx fy cx cy W H, ref/kf/cur pose[7], n_ref n_kf, then per feature
 //                                  px[2] bearing[3] point[3] has_point; prints "err status pose[7]" per call
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -185,6 +186,19 @@ int main(int argc, char** argv) {
                 std::printf("%.17g %d", e, align.lastStatus());
                 for (double x : cur->m_absPose) std::printf(" %.17g", x);
                 std::printf("\n");
+            }
+            // REPS > 0: the per-frame latency of align() as src/system.cpp:313 pays it (median of REPS calls)
+            const int reps = argc >= 11 ? std::atoi(argv[10]) : 0;
+            if (reps > 0) {
+                std::vector<double> ms;
+                for (int i = 0; i < reps; ++i) {
+                    cur->m_absPose = poses[2];
+                    const auto t0 = std::chrono::steady_clock::now();
+                    align.align(ref, cur);
+                    ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+                }
+                std::sort(ms.begin(), ms.end());
+                std::printf("ms %.6f\n", ms[ms.size() / 2]);
             }
             return 0;
         }

@@ -254,6 +254,24 @@ def map_objects(p, levels=1, ctx=None, seed=0):
     return m, ref, kf, cur, points, feats
 
 
+def write_align_problem(s, directory):
+    """Files for build/svo_host_check align (the C++ mirror's ImageAlignment): align.bin (the camera, the three
+    poses, n_ref, n_kf, then one 9-double row per feature: px, bearing, point, has_point) and the three base
+    images.  Returns the four paths."""
+    c = s.camera
+    hdr = [c["fx"], c["fy"], c["cx"], c["cy"], c["width"], c["height"], *s.ref_pose, *s.kf_pose, *s.cur_init_pose,
+           s.n_ref, s.n_kf]
+    rows = np.concatenate([s.px, s.bearing, s.point, s.has_point.reshape(-1, 1).astype(np.float64)], axis=1)
+    data = os.path.join(directory, "align.bin")
+    np.concatenate([np.array(hdr, np.float64), rows.ravel()]).tofile(data)
+    paths = [data]
+    for k, img in (("ref", s.ref_img), ("kf", s.kf_img), ("cur", s.cur_img)):
+        path = os.path.join(directory, f"{k}.raw")
+        np.ascontiguousarray(img, np.uint8).tofile(path)
+        paths.append(path)
+    return paths
+
+
 def write_map_problem(p, directory, cell_order):
     """Files for build/svo_host_check map (the C++ mirror's Map): DATA.bin (doubles, layout in
     host/svo_host_check.cpp) and the three base images.  Returns the four paths."""
