@@ -64,6 +64,7 @@ struct VShared {
     uint4 rec[kSteps];                // per step of the round: GE lo, GE hi, LE lo, LE hi
     uint32_t pre[kSteps];             // per step: #GE | #LE << 16 before it (each wave writes its own steps)
     double pub[6];                    // pre-values published by their owners (candidates 0-3, record 4)
+    uint32_t pubk[4];                 // the candidates' target ranks (0: not a target), by their owners
     double bcd;                       // broadcast of the median between the passes
     double lrow[R - kVRegRows][kVT];  // rows 88..97 of the vector (the rest is in registers)
     uint32_t tmp[2 * kVW];            // per-wave counts of the prologue
@@ -407,6 +408,30 @@ struct VSel {
         if (((q >> 6) & (kVW - 1)) != (uint32_t)wave) return;
         const double x = row_val((int)(q >> 9));
         if ((uint32_t)lane == (q & 63u)) sh.pub[slot] = x;
+    }
+    // candidate q of the next round (slot i): its owner publishes the pre-value and, if q is one of this round's
+    // swap targets (side: 0 GE ranked from the left, 1 LE ranked from the right, rank <= ks), its rank, from the
+    // step's record (masked to the round's segment at the classification) and the step's prefix (written by
+    // this same wave in the scan)
+    __device__ __forceinline__ void publish_cand(uint32_t q, int i, uint32_t ks, int side, uint32_t totL) {
+        if (((q >> 6) & (kVW - 1)) != (uint32_t)wave) return;
+        const double x = row_val((int)(q >> 9));
+        uint32_t k = 0;
+        if (ks) {
+            const uint32_t s = q >> 6, b = q & 63u;
+            const uint4 m4 = sh.rec[s];
+            const uint64_t m = side ? ((uint64_t)uni(m4.w) << 32) | uni(m4.z) : ((uint64_t)uni(m4.y) << 32) | uni(m4.x);
+            if ((m >> b) & 1ull) {
+                const uint32_t pp = uni(sh.pre[s]);
+                const uint32_t below = popc(m & low_mask(b));
+                k = side ? totL - ((pp >> 16) + below) : (pp & 0xFFFFu) + below + 1u;
+                if (k > ks) k = 0;
+            }
+        }
+        if ((uint32_t)lane == (q & 63u)) {
+            sh.pub[i] = x;
+            sh.pubk[i] = k;
+        }
     }
     // positions [f, l) -> dst[q - dbase]; the other lanes store to dummy + lane (branch-free)
     __device__ __forceinline__ void dump(double* dst, uint32_t dbase, double* dummy) {
@@ -762,22 +787,20 @@ struct VSel {
         const uint32_t nS = nl - nf;
         const bool need = nS > kOneWave && depth > 0;  // another block round follows
         const uint32_t cq[4] = {nf + 1u, nf + nS / 2u, nl - 1u, nf};
-        if (need) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) publish(cq[i], i);
-        }
         // sources: the side the kept side takes its values from; targets: the kept side's swapped positions
         const int src_side = right ? 0 : 1, tgt_side = right ? 1 : 0;
+        // the next round's candidates: each owner publishes its pre-value and its target rank (the mailbox
+        // slot that will hold its new value), from its own step's prefix and record; the other waves do nothing
+        if (need) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) publish_cand(cq[i], i, ks, tgt_side, totL);
+        }
         const uint32_t sl = (l - 1) >> 6;
         const uint32_t s0L = S.sf, s1L = lk != kNone ? lk >> 6 : 0u;           // L_k, k <= Ks
         const uint32_t s0R = rk != kNone ? rk >> 6 : sl + 1u, s1R = sl;       // R_k, k <= Ks
         // Ks beyond the mailbox: chunks of kMbCap ranks, the masks from the records (see exchange).
         const uint32_t nch = ks == 0 ? 1u : (ks + kMbCap - 1u) / kMbCap;
         uint32_t ck[4] = {0, 0, 0, 0};  // the candidates' target ranks (0: not a target)
-        if (need && ks) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ck[i] = side_rank(S, cq[i], tgt_side, ks, totL);
-        }
         VSTAMP(3);
         for (uint32_t it = 0; it < nch; ++it) {
             const uint32_t ci = it;
@@ -793,7 +816,10 @@ struct VSel {
                 if (record) { lo_val = uni(sh.pub[4]); rec = true; }
                 if (need) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) cand[i] = uni(sh.pub[i]);
+                    for (int i = 0; i < 4; ++i) {
+                        cand[i] = uni(sh.pub[i]);
+                        ck[i] = uni(sh.pubk[i]);
+                    }
                 }
             }
             if (ks) {
