@@ -556,6 +556,7 @@ struct VSel {
         // an and-or chain in asm (one v_and_or_b32 per slot): written as plain selects, the compiler turned it
         // into an indexed load and kept pk[] in scratch memory (a store per entry every scan, a memory round
         // trip per lookup)
+        if (S.K == 1) return uni(lane_read(S.pk[0], (int)e));  // (one entry per lane: most rounds)
         uint32_t x = 0;
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
@@ -592,19 +593,6 @@ struct VSel {
         const uint32_t l2 = lcar - popc(le & low_mask(lo));
         return g1 > l2 ? g1 : l2;
     }
-    // the rank (1-based) of position q among the round's swap targets of a side, 0 if it is none
-    // (side 0: GE ranked from the left, side 1: LE ranked from the right).  From the scan registers and the
-    // records, so it runs before the mailbox barrier: after it, a fast wave's next classification may
-    // already overwrite the records.
-    __device__ __forceinline__ uint32_t side_rank(const Scan& S, uint32_t q, int side, uint32_t ks, uint32_t totL) const {
-        const uint32_t s = q >> 6, b = q & 63u;
-        const uint64_t m = rec_mask(s, side);
-        const uint32_t pp = pk_at(S, s - S.sf);
-        if (!((m >> b) & 1ull)) return 0;
-        const uint32_t k = side ? totL - ((pp >> 16) + popc(m & low_mask(b))) : (pp & 0xFFFFu) + popc(m & low_mask(b)) + 1u;
-        return k <= ks ? k : 0u;
-    }
-
     // ------------------------------------------------------------------ 3. the exchange
     // side 0: GE positions ranked from the left (L_k), side 1: LE positions ranked from the right (R_k), over
     // the steps [s0, s1]; ranks k in (k0, k1]: kWrite stores the value in mb[k - 1 - k0], else the position
@@ -612,14 +600,17 @@ struct VSel {
     // chunked (more than one exchange chunk): the masks come from the records instead, since an earlier
     // chunk's targets may have changed registers the recompute would read (the round then ends with a barrier,
     // so no wave reads the records while a faster one classifies the next round)
+    // this wave's step prefixes, lane j: row j (pre0) and row 64 + j (pre1), read once per round for both
+    // exchange phases
+    __device__ __forceinline__ void wave_prefixes(uint32_t& pre0, uint32_t& pre1) const {
+        pre0 = sh.pre[((uint32_t)lane * kVW + (uint32_t)wave) % kSteps];
+        pre1 = sh.pre[(((uint32_t)lane + 64u) * kVW + (uint32_t)wave) % kSteps];
+    }
     template <bool kWrite>
     __device__ __forceinline__ void exchange(int side, uint32_t s0, uint32_t s1, double p, uint32_t totL, uint32_t k0,
-                                             uint32_t k1, bool chunked) {
+                                             uint32_t k1, bool chunked, uint32_t pre0, uint32_t pre1) {
         const WaveRows w = wave_segment(s0, s1);
         if (w.rlo > w.rhi) return;
-        // this wave's step prefixes, lane j: row j (and row 64 + j): one LDS read each, then readlanes
-        const uint32_t pre0 = sh.pre[((uint32_t)lane * kVW + (uint32_t)wave) % kSteps];
-        const uint32_t pre1 = sh.pre[(((uint32_t)lane + 64u) * kVW + (uint32_t)wave) % kSteps];
         // a lane's mailbox index: ranks k0 < k <= k1 of m (okm) use mbx[k - 1 - k0], the other lanes their
         // dummy slot mbx[kMbCap + lane].  kk = k - 1 - k0 is one mbcnt over a scalar base (side 0: ranks from
         // the left, pp's GE count + the GE lanes below + 1; side 1: ranks from the right, totL - (pp's LE
@@ -801,13 +792,15 @@ struct VSel {
         // Ks beyond the mailbox: chunks of kMbCap ranks, the masks from the records (see exchange).
         const uint32_t nch = ks == 0 ? 1u : (ks + kMbCap - 1u) / kMbCap;
         uint32_t ck[4] = {0, 0, 0, 0};  // the candidates' target ranks (0: not a target)
+        uint32_t pre0 = 0, pre1 = 0;
+        if (ks) wave_prefixes(pre0, pre1);
         VSTAMP(3);
         for (uint32_t it = 0; it < nch; ++it) {
             const uint32_t ci = it;
             const uint32_t k0 = ci * kMbCap, k1 = ks < k0 + kMbCap ? ks : k0 + kMbCap;
             if (ks) {
-                if (src_side == 0) exchange<true>(0, s0L, s1L, p, totL, k0, k1, nch > 1);
-                else exchange<true>(1, s0R, s1R, p, totL, k0, k1, nch > 1);
+                if (src_side == 0) exchange<true>(0, s0L, s1L, p, totL, k0, k1, nch > 1, pre0, pre1);
+                else exchange<true>(1, s0R, s1R, p, totL, k0, k1, nch > 1, pre0, pre1);
             }
             VSTAMP(4);
             __syncthreads();
@@ -823,8 +816,8 @@ struct VSel {
                 }
             }
             if (ks) {
-                if (tgt_side == 0) exchange<false>(0, s0L, s1L, p, totL, k0, k1, nch > 1);
-                else exchange<false>(1, s0R, s1R, p, totL, k0, k1, nch > 1);
+                if (tgt_side == 0) exchange<false>(0, s0L, s1L, p, totL, k0, k1, nch > 1, pre0, pre1);
+                else exchange<false>(1, s0R, s1R, p, totL, k0, k1, nch > 1, pre0, pre1);
                 if (need) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
