@@ -751,23 +751,40 @@ struct VSel {
         }
         const uint32_t es = uni(wave_sum_u(c)) - 1u;
         const uint32_t pke = pk_at(S, es);
-        const uint32_t ks = uni(wave_crossing_ks(pke & 0xFFFFu, totL - (pke >> 16), rec_mask(S.sf + es, 0), rec_mask(S.sf + es, 1)));
+        const uint4 me4 = sh.rec[S.sf + es];  // (both masks of the crossing entry in one read)
+        const uint64_t mge = ((uint64_t)uni(me4.y) << 32) | uni(me4.x), mle = ((uint64_t)uni(me4.w) << 32) | uni(me4.z);
+        const uint32_t ks = uni(wave_crossing_ks(pke & 0xFFFFu, totL - (pke >> 16), mge, mle));
         VSTAMP(9);
-        // L_{Ks+1} (GE rank Ks + 1), R_{Ks} (LE rank totL - Ks + 1 from the left), L_{Ks}: one packed count
+        // L_{Ks+1} (GE rank Ks + 1), R_{Ks} (LE rank totL - Ks + 1 from the left), L_{Ks}.  All three sit next to
+        // the crossing split, so they are looked for in the crossing entry first (its prefix and masks are at
+        // hand); only if one of them lies in another entry do the ranks take the full search (a packed count
+        // over every entry, then a lookup and a bit select per rank).
         const uint32_t ra = ks + 1u, rb = totL - ks + 1u, rc = ks;
-        c = 0;
+        const uint32_t G0 = pke & 0xFFFFu, L0 = pke >> 16, cg = popc(mge), cl = popc(mle);
+        const uint32_t ebase = (S.sf + es) * 64u;
+        const bool in_a = ra > totG || (ra > G0 && ra <= G0 + cg);
+        const bool in_b = ks == 0 || (rb > L0 && rb <= L0 + cl);
+        const bool in_c = ks == 0 || (rc > G0 && rc <= G0 + cg);
+        uint32_t lk1, rk, lk;
+        if (in_a && in_b && in_c) {
+            lk1 = ra <= totG ? ebase + uni(wave_select_bit(mge, ra - G0 - 1u)) : kNone;
+            rk = ks >= 1 ? ebase + uni(wave_select_bit(mle, rb - L0 - 1u)) : kNone;
+            lk = ks >= 1 ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : kNone;
+        } else {
+            c = 0;
 #pragma unroll
-        for (int i = 0; i < kKl; ++i) {
-            const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
-            if ((uint32_t)i < S.K && e < S.E) {
-                const uint32_t pg = S.pk[i] & 0xFFFFu, pl = S.pk[i] >> 16;
-                c += (pg < ra ? 1u : 0u) + (pl < rb ? 1u << 10 : 0u) + (pg < rc ? 1u << 20 : 0u);
+            for (int i = 0; i < kKl; ++i) {
+                const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
+                if ((uint32_t)i < S.K && e < S.E) {
+                    const uint32_t pg = S.pk[i] & 0xFFFFu, pl = S.pk[i] >> 16;
+                    c += (pg < ra ? 1u : 0u) + (pl < rb ? 1u << 10 : 0u) + (pg < rc ? 1u << 20 : 0u);
+                }
             }
+            const uint32_t cs = uni(wave_sum_u(c));
+            lk1 = ra <= totG ? uni(locate(S, cs & 1023u, 0, ra)) : kNone;
+            rk = ks >= 1 ? uni(locate(S, (cs >> 10) & 1023u, 1, rb)) : kNone;
+            lk = ks >= 1 ? uni(locate(S, cs >> 20, 0, rc)) : kNone;
         }
-        const uint32_t cs = uni(wave_sum_u(c));
-        const uint32_t lk1 = ra <= totG ? uni(locate(S, cs & 1023u, 0, ra)) : kNone;
-        const uint32_t rk = ks >= 1 ? uni(locate(S, (cs >> 10) & 1023u, 1, rb)) : kNone;
-        const uint32_t lk = ks >= 1 ? uni(locate(S, cs >> 20, 0, rc)) : kNone;
         const uint32_t cut = lk1 < rk ? lk1 : rk;
         VSTAMP(10);
         const bool right = cut <= nth;  // the side introselect continues with
