@@ -519,26 +519,41 @@ struct VSel {
         S.sf = f >> 6;
         S.E = ((l - 1) >> 6) - S.sf + 1;
         S.K = (S.E + 63u) >> 6;
-        uint32_t tg = 0, tl = 0;
+        // #GE | #LE << 16 packed in one word (both <= 50 176: the low half never carries into the high one), so
+        // one DPP scan serves both counts
+        if (S.K == 1) {  // one entry per lane (segments of <= 4096 positions): no slot loops
+            const uint32_t e = (uint32_t)lane;
+            uint32_t c = 0;
+            if (e < S.E) {
+                const uint4 m = sh.rec[S.sf + e];
+                c = ((uint32_t)__popc(m.x) + (uint32_t)__popc(m.y)) | (((uint32_t)__popc(m.z) + (uint32_t)__popc(m.w)) << 16);
+            }
+            const uint32_t it = wave_incl_scan(c);
+            S.pk[0] = it - c;
+            if (e < S.E && ((S.sf + e) & (kVW - 1)) == (uint32_t)wave) sh.pre[S.sf + e] = S.pk[0];
+            const uint32_t tot = uni(lane_read(it, 63));
+            S.totG = tot & 0xFFFFu;
+            S.totL = tot >> 16;
+            return;
+        }
+        uint32_t t = 0;
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
             S.pk[i] = 0;
             if ((uint32_t)i < S.K) {
                 const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
-                uint32_t cg = 0, cl = 0;
+                uint32_t c = 0;
                 if (e < S.E) {
                     const uint4 m = sh.rec[S.sf + e];
-                    cg = (uint32_t)__popc(m.x) + (uint32_t)__popc(m.y);
-                    cl = (uint32_t)__popc(m.z) + (uint32_t)__popc(m.w);
+                    c = ((uint32_t)__popc(m.x) + (uint32_t)__popc(m.y)) | (((uint32_t)__popc(m.z) + (uint32_t)__popc(m.w)) << 16);
                 }
-                S.pk[i] = tg | (tl << 16);
-                tg += cg;
-                tl += cl;
+                S.pk[i] = t;
+                t += c;
                 if ((i & (kScanGroup - 1)) == kScanGroup - 1) asm volatile("" ::: "memory");  // bounded reads in flight
             }
         }
-        const uint32_t ig = wave_incl_scan(tg), il = wave_incl_scan(tl);
-        const uint32_t off = (ig - tg) | ((il - tl) << 16);
+        const uint32_t it = wave_incl_scan(t);
+        const uint32_t off = it - t;
 #pragma unroll
         for (int i = 0; i < kKl; ++i) {
             if ((uint32_t)i < S.K) {
@@ -547,8 +562,9 @@ struct VSel {
                 if (e < S.E && ((S.sf + e) & (kVW - 1)) == (uint32_t)wave) sh.pre[S.sf + e] = S.pk[i];
             }
         }
-        S.totG = uni(lane_read(ig, 63));
-        S.totL = uni(lane_read(il, 63));
+        const uint32_t tot = uni(lane_read(it, 63));
+        S.totG = tot & 0xFFFFu;
+        S.totL = tot >> 16;
     }
     // the packed prefix of a block-uniform entry
     __device__ __forceinline__ uint32_t pk_at(const Scan& S, uint32_t e) const {
@@ -743,13 +759,17 @@ struct VSel {
         VSTAMP(8);
         const uint32_t totL = S.totL, totG = S.totG;
         // the crossing: the last entry whose start has G < Lc (entry 0 always: G = 0 < Lc = totL)
-        uint32_t c = 0;
+        uint32_t c = 0, es;
+        if (S.K == 1) {  // one entry per lane: a ballot counts them
+            es = popc(__ballot((uint32_t)lane < S.E && (S.pk[0] & 0xFFFFu) < totL - (S.pk[0] >> 16))) - 1u;
+        } else {
 #pragma unroll
-        for (int i = 0; i < kKl; ++i) {
-            const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
-            if ((uint32_t)i < S.K && e < S.E) c += (S.pk[i] & 0xFFFFu) < totL - (S.pk[i] >> 16) ? 1u : 0u;
+            for (int i = 0; i < kKl; ++i) {
+                const uint32_t e = (uint32_t)lane * S.K + (uint32_t)i;
+                if ((uint32_t)i < S.K && e < S.E) c += (S.pk[i] & 0xFFFFu) < totL - (S.pk[i] >> 16) ? 1u : 0u;
+            }
+            es = uni(wave_sum_u(c)) - 1u;
         }
-        const uint32_t es = uni(wave_sum_u(c)) - 1u;
         const uint32_t pke = pk_at(S, es);
         const uint4 me4 = sh.rec[S.sf + es];  // (both masks of the crossing entry in one read)
         const uint64_t mge = ((uint64_t)uni(me4.y) << 32) | uni(me4.x), mle = ((uint64_t)uni(me4.w) << 32) | uni(me4.z);
