@@ -314,6 +314,16 @@ __device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b)
     asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
     return r;
 }
+// x with lane j (a block-uniform, dynamic lane) replaced by v: a compare and a v_cndmask (the compiler's
+// v_writelane with a dynamic lane goes through M0, which the row moves overwrite)
+__device__ __forceinline__ uint32_t lane_put(uint32_t x, uint32_t v, uint32_t j, uint32_t me) {
+    uint32_t r;
+    uint64_t eq;
+    asm("v_cmp_eq_u32_e64 %1, %2, %3\n\tv_cndmask_b32_e64 %0, %4, %5, %1"
+        : "=v"(r), "=&s"(eq)
+        : "v"(me), "s"(j), "v"(x), "v"(v));
+    return r;
+}
 // rows 0..87 of src (positions 512 r + tid) into the data VGPRs; lanes past `bytes` read 0 (buffer range)
 __device__ __forceinline__ void vload(const double* src, uint32_t bytes, int tid) {
     const uint64_t a = (uint64_t)src;
@@ -896,6 +906,8 @@ struct VSel {
         // the mailbox and each lane's dummy slot as indices into sh.mbx
         const uint32_t mb0 = (uint32_t)(mb - sh.mbx), dslot = kMbCap + me;
         double* const mbx = sh.mbx;
+        // per-step data of a round in VGPR lanes (lane j = step j): the GE / LE masks and the #GE / #LE before
+        // the step; the loops run over the live steps js..je only and the searches are ballots over the lanes
         while (lr - fr > 3 && depth > 0) {
             --depth;
             ++nrounds;
@@ -908,46 +920,49 @@ struct VSel {
             vsel((int)(fr >> 6), pe, 1ull << (fr & 63u));
             vsel((int)(chh >> 6), xv, 1ull << (chh & 63u));
             const uint32_t js = fr >> 6, je = (lr - 1) >> 6;
-            double w[8];
-            uint64_t ge[8], le[8];
-            uint32_t gp[8], lp[8];  // #GE / #LE before each step
+            uint32_t gel = 0, geh = 0, lel = 0, leh = 0, pkv = 0;  // lane j: step j's masks, packed #GE | #LE << 16 before it
             uint32_t tG = 0, tL = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                ge[j] = le[j] = 0;
-                w[j] = 0.0;
-                if ((uint32_t)j >= js && (uint32_t)j <= je) {
-                    const uint32_t base = 64u * (uint32_t)j;
-                    w[j] = vget(j);
-                    const uint32_t lo = fr > base ? (fr - base < 64u ? fr - base : 64u) : 0u;
-                    const uint32_t hi = lr > base ? (lr - base < 64u ? lr - base : 64u) : 0u;
-                    const uint64_t inm = low_mask(hi) & ~low_mask(lo);
-                    const uint64_t fb = (fr >> 6) == (uint32_t)j ? 1ull << (fr & 63u) : 0ull;
-                    ge[j] = __ballot(!(w[j] < pe)) & inm & ~fb;
-                    le[j] = __ballot(!(pe < w[j])) & inm;
-                }
-                gp[j] = tG;
-                lp[j] = tL;
-                tG += popc(ge[j]);
-                tL += popc(le[j]);
+            for (uint32_t j = js; j <= je; ++j) {
+                uint64_t ge, le;
+                vcmp2((int)j, pe, ge, le);
+                const uint32_t base = 64u * j;
+                const uint32_t lo = fr > base ? fr - base : 0u;
+                const uint32_t hi = lr - base < 64u ? lr - base : 64u;
+                const uint64_t inm = low_mask(hi) & ~low_mask(lo);
+                const uint64_t fb = js == j ? 1ull << (fr & 63u) : 0ull;
+                ge &= inm & ~fb;
+                le &= inm;
+                gel = lane_put(gel, (uint32_t)ge, j, me);
+                geh = lane_put(geh, (uint32_t)(ge >> 32), j, me);
+                lel = lane_put(lel, (uint32_t)le, j, me);
+                leh = lane_put(leh, (uint32_t)(le >> 32), j, me);
+                pkv = lane_put(pkv, tG | (tL << 16), j, me);
+                tG += popc(ge);
+                tL += popc(le);
             }
-            // crossing: the last step whose start has G < Lc (step js: G = 0 < Lc)
-            uint32_t gcar = 0, lcar = tL;
-            uint64_t a0 = 0, b0m = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if ((uint32_t)j >= js && (uint32_t)j <= je && gp[j] < tL - lp[j]) { gcar = gp[j]; lcar = tL - lp[j]; a0 = ge[j]; b0m = le[j]; }
-            const uint32_t ks = uni(wave_crossing_ks(gcar, lcar, a0, b0m));
-            auto rank_pos = [&](int kind, uint32_t rank) -> uint32_t {  // the last step starting below the rank
+            const bool live = me >= js && me <= je;
+            const uint32_t gpl = pkv & 0xFFFFu, lpl = pkv >> 16;
+            auto masks = [&](uint32_t j, uint64_t& ge, uint64_t& le) __attribute__((always_inline)) {
+                ge = ((uint64_t)lane_read(geh, (int)j) << 32) | lane_read(gel, (int)j);
+                le = ((uint64_t)lane_read(leh, (int)j) << 32) | lane_read(lel, (int)j);
+            };
+            // crossing: the last live step whose start has G < Lc (step js: G = 0 < Lc)
+            const uint64_t cq = __ballot(live && gpl < tL - lpl);
+            const uint32_t jc = 63u - (uint32_t)__builtin_clzll(cq);
+            uint64_t a0, b0m;
+            masks(jc, a0, b0m);
+            const uint32_t pkc = lane_read(pkv, (int)jc);
+            const uint32_t ks = uni(wave_crossing_ks(pkc & 0xFFFFu, tL - (pkc >> 16), a0, b0m));
+            // the rank-th GE (kind 0) / LE (kind 1) position: the last live step starting below the rank
+            auto rank_pos = [&](int kind, uint32_t rank) __attribute__((always_inline)) -> uint32_t {
                 if (rank == 0 || rank > (kind ? tL : tG)) return kNone;
-                uint32_t pre = 0, jj = 0;
-                uint64_t mk = 0;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const uint32_t pj = kind ? lp[j] : gp[j];
-                    if ((uint32_t)j >= js && (uint32_t)j <= je && pj < rank) { pre = pj; jj = (uint32_t)j; mk = kind ? le[j] : ge[j]; }
-                }
-                return 64u * jj + wave_select_bit(mk, rank - pre - 1u);
+                const uint64_t q = __ballot(live && (kind ? lpl : gpl) < rank);
+                const uint32_t jj = 63u - (uint32_t)__builtin_clzll(q);
+                const uint32_t pp = lane_read(pkv, (int)jj);
+                const uint32_t pre = kind ? pp >> 16 : pp & 0xFFFFu;
+                uint64_t ge, le;
+                masks(jj, ge, le);
+                return 64u * jj + wave_select_bit(kind ? le : ge, rank - pre - 1u);
             };
             const uint32_t lk1 = rank_pos(0, ks + 1), rk = ks >= 1 ? rank_pos(1, tL - ks + 1) : kNone;
             const uint32_t cut = lk1 < rk ? lk1 : rk;
@@ -958,22 +973,26 @@ struct VSel {
                 rec = true;
             }
             // sources to the mailbox, then the kept side's targets take it (masked selects into the rows)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if ((uint32_t)j < js || (uint32_t)j > je) continue;
-                const uint64_t m = right ? ge[j] : le[j];
-                const uint32_t k = right ? gp[j] + lanes_below(m) + 1u : tL - (lp[j] + lanes_below(m));
-                const uint64_t okm = m & __ballot(k <= ks);
-                mbx[lane_sel(okm, mb0 + k - 1u, dslot)] = w[j];
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if ((uint32_t)j < js || (uint32_t)j > je) continue;
-                const uint64_t m = right ? le[j] : ge[j];
-                const uint32_t k = right ? tL - (lp[j] + lanes_below(m)) : gp[j] + lanes_below(m) + 1u;
-                const uint64_t okm = m & __ballot(k <= ks);
-                const double t = mbx[lane_sel(okm, mb0 + k - 1u, dslot)];
-                vsel(j, t, okm);
+            if (ks) {
+                for (uint32_t j = js; j <= je; ++j) {
+                    uint64_t ge, le;
+                    masks(j, ge, le);
+                    const uint64_t m = right ? ge : le;
+                    const uint32_t pp = lane_read(pkv, (int)j);
+                    const uint32_t k = right ? (pp & 0xFFFFu) + lanes_below(m) + 1u : tL - ((pp >> 16) + lanes_below(m));
+                    const uint64_t okm = m & __ballot(k <= ks);
+                    mbx[lane_sel(okm, mb0 + k - 1u, dslot)] = vget((int)j);
+                }
+                for (uint32_t j = js; j <= je; ++j) {
+                    uint64_t ge, le;
+                    masks(j, ge, le);
+                    const uint64_t m = right ? le : ge;
+                    const uint32_t pp = lane_read(pkv, (int)j);
+                    const uint32_t k = right ? tL - ((pp >> 16) + lanes_below(m)) : (pp & 0xFFFFu) + lanes_below(m) + 1u;
+                    const uint64_t okm = m & __ballot(k <= ks);
+                    const double t = mbx[lane_sel(okm, mb0 + k - 1u, dslot)];
+                    vsel((int)j, t, okm);
+                }
             }
             if (right) fr = cut;
             else lr = cut;
