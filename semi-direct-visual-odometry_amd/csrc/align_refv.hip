@@ -47,7 +47,11 @@ constexpr int kVRegRows = 88;         // rows in v80..v255; rows 88..97 in LDS (
 static_assert(kVBase + 2 * kVRegRows == 256, "register rows fill v80..v255");
 constexpr uint32_t kVCap = (uint32_t)kVRows * kVT;
 constexpr uint32_t kMbCap = 12288;    // mailbox (doubles); Ks beyond it exchanges in chunks
-constexpr uint32_t kOneWave = 512;    // segments of <= 512 positions continue on wave 0
+#ifndef SVO_ONEWAVE
+#define SVO_ONEWAVE 512
+#endif
+constexpr uint32_t kOneWave = SVO_ONEWAVE;  // segments of <= kOneWave positions continue on wave 0
+static_assert(kOneWave % 64 == 0 && kOneWave / 64 <= kVRegRows && 2 * kOneWave <= kMbCap, "one-wave segment rows");
 #if defined(SVO_STAMPS)
 constexpr int kScanGroup = 2;         // record reads the scan keeps in flight (the stamps cost registers)
 #else
@@ -902,7 +906,7 @@ struct VSel {
         uint32_t fr = 0, lr = l - f;
         const uint32_t nrel = nth - f0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) vset(j, seg[64 * j + lane]);
+        for (int j = 0; j < (int)(kOneWave / 64); ++j) vset(j, seg[64 * j + lane]);
         // the mailbox and each lane's dummy slot as indices into sh.mbx
         const uint32_t mb0 = (uint32_t)(mb - sh.mbx), dslot = kMbCap + me;
         double* const mbx = sh.mbx;
@@ -998,7 +1002,7 @@ struct VSel {
             else lr = cut;
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) seg[64 * j + lane] = vget(j);
+        for (int j = 0; j < (int)(kOneWave / 64); ++j) seg[64 * j + lane] = vget(j);
         f = f0 + fr;
         l = f0 + lr;
     }
