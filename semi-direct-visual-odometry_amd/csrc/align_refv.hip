@@ -799,12 +799,8 @@ struct VSel {
         const bool in_a = ra > totG || (ra > G0 && ra <= G0 + cg);
         const bool in_b = ks == 0 || (rb > L0 && rb <= L0 + cl);
         const bool in_c = ks == 0 || (rc > G0 && rc <= G0 + cg);
-        uint32_t lk1, rk, lk;
-        if (in_a && in_b && in_c) {
-            lk1 = ra <= totG ? ebase + uni(wave_select_bit(mge, ra - G0 - 1u)) : kNone;
-            rk = ks >= 1 ? ebase + uni(wave_select_bit(mle, rb - L0 - 1u)) : kNone;
-            lk = ks >= 1 ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : kNone;
-        } else {
+        uint32_t cs = 0;  // the packed count of every entry below each rank, only when a rank lies elsewhere
+        if (!(in_a && in_b && in_c)) {
             c = 0;
 #pragma unroll
             for (int i = 0; i < kKl; ++i) {
@@ -814,11 +810,14 @@ struct VSel {
                     c += (pg < ra ? 1u : 0u) + (pl < rb ? 1u << 10 : 0u) + (pg < rc ? 1u << 20 : 0u);
                 }
             }
-            const uint32_t cs = uni(wave_sum_u(c));
-            lk1 = ra <= totG ? uni(locate(S, cs & 1023u, 0, ra)) : kNone;
-            rk = ks >= 1 ? uni(locate(S, (cs >> 10) & 1023u, 1, rb)) : kNone;
-            lk = ks >= 1 ? uni(locate(S, cs >> 20, 0, rc)) : kNone;
+            cs = uni(wave_sum_u(c));
         }
+        const uint32_t lk1 = ra > totG ? kNone
+                             : in_a ? ebase + uni(wave_select_bit(mge, ra - G0 - 1u)) : uni(locate(S, cs & 1023u, 0, ra));
+        const uint32_t rk = ks == 0 ? kNone
+                            : in_b ? ebase + uni(wave_select_bit(mle, rb - L0 - 1u)) : uni(locate(S, (cs >> 10) & 1023u, 1, rb));
+        const uint32_t lk = ks == 0 ? kNone
+                            : in_c ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : uni(locate(S, cs >> 20, 0, rc));
         const uint32_t cut = lk1 < rk ? lk1 : rk;
         VSTAMP(10);
         const bool right = cut <= nth;  // the side introselect continues with
