@@ -318,6 +318,16 @@ __device__ __forceinline__ uint32_t lane_sel(uint64_t m, uint32_t a, uint32_t b)
     asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
     return r;
 }
+// one step record (GE mask, LE mask) stored at LDS byte address addr + kOff: two 64-bit moves from the SGPR
+// masks and two 8-B stores (the compiler's form: four 32-bit moves, an address move and a 16-B store)
+template <int kOff>
+__device__ __forceinline__ void rec_put(uint32_t addr, uint64_t ge, uint64_t le) {
+    uint64_t tg, tl;
+    asm volatile("v_mov_b64 %0, %3\n\tv_mov_b64 %1, %4\n\tds_write_b64 %2, %0 offset:%5\n\tds_write_b64 %2, %1 offset:%6"
+                 : "=&v"(tg), "=&v"(tl)
+                 : "v"(addr), "s"(ge), "s"(le), "i"(kOff), "i"(kOff + 8)
+                 : "memory");
+}
 // x with lane j (a block-uniform, dynamic lane) replaced by v: a compare and a v_cndmask (the compiler's
 // v_writelane with a dynamic lane goes through M0, which the row moves overwrite)
 __device__ __forceinline__ uint32_t lane_put(uint32_t x, uint32_t v, uint32_t j, uint32_t me) {
@@ -507,11 +517,18 @@ struct VSel {
         const int ra = w.rlo + 1, rb = w.rhi - 1;  // interior rows
         const int r1 = rb < kVRegRows - 1 ? rb : kVRegRows - 1;
         int r = ra;
+        // LDS byte address of this wave's record of row 0 (row r: + r * 128)
+        const uint32_t rec0 = (uint32_t)(uintptr_t)(recw);
         for (; r + 3 <= r1; r += 4) {
             uint64_t ge[4], le[4];
             vcmp2x4(r, p, ge, le);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) put(r + j, ge[j], le[j]);
+            if (lane == 0) {
+                const uint32_t ad = rec0 + (uint32_t)r * (uint32_t)(kVW * sizeof(uint4));
+                rec_put<0>(ad, ge[0], le[0]);
+                rec_put<kVW * 16>(ad, ge[1], le[1]);
+                rec_put<2 * kVW * 16>(ad, ge[2], le[2]);
+                rec_put<3 * kVW * 16>(ad, ge[3], le[3]);
+            }
         }
         for (; r <= r1; ++r) {
             uint64_t ge, le;
