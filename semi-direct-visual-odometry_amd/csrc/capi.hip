@@ -724,7 +724,9 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     a.fx = b->cam.fx; a.fy = b->cam.fy; a.cx = b->cam.cx; a.cy = b->cam.cy;
     a.geom = b->geom;
     svo_ctx* c = b->ctx;
-    if (marks || b->n_pairs < kSplitMin) {
+    // SVO_CHAINS=1 (measurement knob, read once): the whole batch as one chain
+    static const bool one_chain = getenv("SVO_CHAINS") && atoi(getenv("SVO_CHAINS")) == 1;
+    if (marks || b->n_pairs < kSplitMin || one_chain) {
         svo::launch_align(a, c->stream, marks);
     } else {
         // two independent half-batch chains on two streams: one chain's latency-bound stages (the
