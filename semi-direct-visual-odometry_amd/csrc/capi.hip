@@ -826,9 +826,18 @@ int svo_align_batch_traces(svo_align_batch* b, int32_t pair, svo_level_trace* ou
     if (pair < 0 || pair >= b->n_pairs) return fail(SVO_ERR_ARG, "pair out of range");
     SVO_HIP(hipSetDevice(b->ctx->device));
     const int L = b->params.max_level + 1;
-    SVO_HIP(hipMemcpyAsync(out, b->d_traces + (size_t)pair * L, L * sizeof(svo_level_trace), hipMemcpyDeviceToHost,
-                           b->ctx->stream));
-    SVO_HIP(hipStreamSynchronize(b->ctx->stream));
+    const size_t bytes = L * sizeof(svo_level_trace);
+    svo_ctx* c = b->ctx;
+    void* host = nullptr;
+    if (ctx_pinned(c, bytes, &host) == hipSuccess) {  // a kernel copy through the pinned block (as results)
+        SVO_HIP(stage_copy(c, host, b->d_traces + (size_t)pair * L, bytes, hipMemcpyDeviceToHost, c->stream));
+        SVO_HIP(hipStreamSynchronize(c->stream));
+        std::memcpy(out, host, bytes);
+        return SVO_OK;
+    }
+    (void)hipGetLastError();
+    SVO_HIP(hipMemcpyAsync(out, b->d_traces + (size_t)pair * L, bytes, hipMemcpyDeviceToHost, c->stream));
+    SVO_HIP(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }
 

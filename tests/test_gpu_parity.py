@@ -202,6 +202,10 @@ def test_class_surface_align():
     first = cur.abs_pose.copy()
     cur.abs_pose[:] = s.cur_init_pose
     assert ia.align(ref, cur) == err and np.array_equal(cur.abs_pose, first)
+    # the per-level traces of the last call (entry l: level l), read on first access
+    tr = ia.last_traces
+    assert tr is ia.last_traces and [t.level for t in tr] == [0, 1, 2, 3, 4]
+    assert all(t.n_vis > 0 for t in tr)
     # exact order statistics on request
     cur.abs_pose[:] = s.cur_init_pose
     svo_amd.ImageAlignment(5, 0, 4, median_mode=svo_amd.MEDIAN_EXACT).align(ref, cur)
