@@ -205,6 +205,98 @@ struct VDiag {  // svo_debug_robust_scale diagnostics
     "v_add_u32 %[vt], 0x56000, %[vo]\n\tbuffer_load_dwordx2 v[252:253], %[vt], %[rs], 0 offen\n\t" \
     "v_add_u32 %[vt], 0x57000, %[vo]\n\tbuffer_load_dwordx2 v[254:255], %[vt], %[rs], 0 offen\n\t"
 
+// the MAD pass's |x - med| on the data registers in place (src/algorithm.cpp:860-863): one subtraction and one
+// sign clear per row, no index sessions (the same IEEE result as fabs(x - med))
+#define SVO_VMAD_ASM \
+    "v_add_f64 v[80:81], v[80:81], -%[m]\n\tv_and_b32 v81, 0x7fffffff, v81\n\t" \
+    "v_add_f64 v[82:83], v[82:83], -%[m]\n\tv_and_b32 v83, 0x7fffffff, v83\n\t" \
+    "v_add_f64 v[84:85], v[84:85], -%[m]\n\tv_and_b32 v85, 0x7fffffff, v85\n\t" \
+    "v_add_f64 v[86:87], v[86:87], -%[m]\n\tv_and_b32 v87, 0x7fffffff, v87\n\t" \
+    "v_add_f64 v[88:89], v[88:89], -%[m]\n\tv_and_b32 v89, 0x7fffffff, v89\n\t" \
+    "v_add_f64 v[90:91], v[90:91], -%[m]\n\tv_and_b32 v91, 0x7fffffff, v91\n\t" \
+    "v_add_f64 v[92:93], v[92:93], -%[m]\n\tv_and_b32 v93, 0x7fffffff, v93\n\t" \
+    "v_add_f64 v[94:95], v[94:95], -%[m]\n\tv_and_b32 v95, 0x7fffffff, v95\n\t" \
+    "v_add_f64 v[96:97], v[96:97], -%[m]\n\tv_and_b32 v97, 0x7fffffff, v97\n\t" \
+    "v_add_f64 v[98:99], v[98:99], -%[m]\n\tv_and_b32 v99, 0x7fffffff, v99\n\t" \
+    "v_add_f64 v[100:101], v[100:101], -%[m]\n\tv_and_b32 v101, 0x7fffffff, v101\n\t" \
+    "v_add_f64 v[102:103], v[102:103], -%[m]\n\tv_and_b32 v103, 0x7fffffff, v103\n\t" \
+    "v_add_f64 v[104:105], v[104:105], -%[m]\n\tv_and_b32 v105, 0x7fffffff, v105\n\t" \
+    "v_add_f64 v[106:107], v[106:107], -%[m]\n\tv_and_b32 v107, 0x7fffffff, v107\n\t" \
+    "v_add_f64 v[108:109], v[108:109], -%[m]\n\tv_and_b32 v109, 0x7fffffff, v109\n\t" \
+    "v_add_f64 v[110:111], v[110:111], -%[m]\n\tv_and_b32 v111, 0x7fffffff, v111\n\t" \
+    "v_add_f64 v[112:113], v[112:113], -%[m]\n\tv_and_b32 v113, 0x7fffffff, v113\n\t" \
+    "v_add_f64 v[114:115], v[114:115], -%[m]\n\tv_and_b32 v115, 0x7fffffff, v115\n\t" \
+    "v_add_f64 v[116:117], v[116:117], -%[m]\n\tv_and_b32 v117, 0x7fffffff, v117\n\t" \
+    "v_add_f64 v[118:119], v[118:119], -%[m]\n\tv_and_b32 v119, 0x7fffffff, v119\n\t" \
+    "v_add_f64 v[120:121], v[120:121], -%[m]\n\tv_and_b32 v121, 0x7fffffff, v121\n\t" \
+    "v_add_f64 v[122:123], v[122:123], -%[m]\n\tv_and_b32 v123, 0x7fffffff, v123\n\t" \
+    "v_add_f64 v[124:125], v[124:125], -%[m]\n\tv_and_b32 v125, 0x7fffffff, v125\n\t" \
+    "v_add_f64 v[126:127], v[126:127], -%[m]\n\tv_and_b32 v127, 0x7fffffff, v127\n\t" \
+    "v_add_f64 v[128:129], v[128:129], -%[m]\n\tv_and_b32 v129, 0x7fffffff, v129\n\t" \
+    "v_add_f64 v[130:131], v[130:131], -%[m]\n\tv_and_b32 v131, 0x7fffffff, v131\n\t" \
+    "v_add_f64 v[132:133], v[132:133], -%[m]\n\tv_and_b32 v133, 0x7fffffff, v133\n\t" \
+    "v_add_f64 v[134:135], v[134:135], -%[m]\n\tv_and_b32 v135, 0x7fffffff, v135\n\t" \
+    "v_add_f64 v[136:137], v[136:137], -%[m]\n\tv_and_b32 v137, 0x7fffffff, v137\n\t" \
+    "v_add_f64 v[138:139], v[138:139], -%[m]\n\tv_and_b32 v139, 0x7fffffff, v139\n\t" \
+    "v_add_f64 v[140:141], v[140:141], -%[m]\n\tv_and_b32 v141, 0x7fffffff, v141\n\t" \
+    "v_add_f64 v[142:143], v[142:143], -%[m]\n\tv_and_b32 v143, 0x7fffffff, v143\n\t" \
+    "v_add_f64 v[144:145], v[144:145], -%[m]\n\tv_and_b32 v145, 0x7fffffff, v145\n\t" \
+    "v_add_f64 v[146:147], v[146:147], -%[m]\n\tv_and_b32 v147, 0x7fffffff, v147\n\t" \
+    "v_add_f64 v[148:149], v[148:149], -%[m]\n\tv_and_b32 v149, 0x7fffffff, v149\n\t" \
+    "v_add_f64 v[150:151], v[150:151], -%[m]\n\tv_and_b32 v151, 0x7fffffff, v151\n\t" \
+    "v_add_f64 v[152:153], v[152:153], -%[m]\n\tv_and_b32 v153, 0x7fffffff, v153\n\t" \
+    "v_add_f64 v[154:155], v[154:155], -%[m]\n\tv_and_b32 v155, 0x7fffffff, v155\n\t" \
+    "v_add_f64 v[156:157], v[156:157], -%[m]\n\tv_and_b32 v157, 0x7fffffff, v157\n\t" \
+    "v_add_f64 v[158:159], v[158:159], -%[m]\n\tv_and_b32 v159, 0x7fffffff, v159\n\t" \
+    "v_add_f64 v[160:161], v[160:161], -%[m]\n\tv_and_b32 v161, 0x7fffffff, v161\n\t" \
+    "v_add_f64 v[162:163], v[162:163], -%[m]\n\tv_and_b32 v163, 0x7fffffff, v163\n\t" \
+    "v_add_f64 v[164:165], v[164:165], -%[m]\n\tv_and_b32 v165, 0x7fffffff, v165\n\t" \
+    "v_add_f64 v[166:167], v[166:167], -%[m]\n\tv_and_b32 v167, 0x7fffffff, v167\n\t" \
+    "v_add_f64 v[168:169], v[168:169], -%[m]\n\tv_and_b32 v169, 0x7fffffff, v169\n\t" \
+    "v_add_f64 v[170:171], v[170:171], -%[m]\n\tv_and_b32 v171, 0x7fffffff, v171\n\t" \
+    "v_add_f64 v[172:173], v[172:173], -%[m]\n\tv_and_b32 v173, 0x7fffffff, v173\n\t" \
+    "v_add_f64 v[174:175], v[174:175], -%[m]\n\tv_and_b32 v175, 0x7fffffff, v175\n\t" \
+    "v_add_f64 v[176:177], v[176:177], -%[m]\n\tv_and_b32 v177, 0x7fffffff, v177\n\t" \
+    "v_add_f64 v[178:179], v[178:179], -%[m]\n\tv_and_b32 v179, 0x7fffffff, v179\n\t" \
+    "v_add_f64 v[180:181], v[180:181], -%[m]\n\tv_and_b32 v181, 0x7fffffff, v181\n\t" \
+    "v_add_f64 v[182:183], v[182:183], -%[m]\n\tv_and_b32 v183, 0x7fffffff, v183\n\t" \
+    "v_add_f64 v[184:185], v[184:185], -%[m]\n\tv_and_b32 v185, 0x7fffffff, v185\n\t" \
+    "v_add_f64 v[186:187], v[186:187], -%[m]\n\tv_and_b32 v187, 0x7fffffff, v187\n\t" \
+    "v_add_f64 v[188:189], v[188:189], -%[m]\n\tv_and_b32 v189, 0x7fffffff, v189\n\t" \
+    "v_add_f64 v[190:191], v[190:191], -%[m]\n\tv_and_b32 v191, 0x7fffffff, v191\n\t" \
+    "v_add_f64 v[192:193], v[192:193], -%[m]\n\tv_and_b32 v193, 0x7fffffff, v193\n\t" \
+    "v_add_f64 v[194:195], v[194:195], -%[m]\n\tv_and_b32 v195, 0x7fffffff, v195\n\t" \
+    "v_add_f64 v[196:197], v[196:197], -%[m]\n\tv_and_b32 v197, 0x7fffffff, v197\n\t" \
+    "v_add_f64 v[198:199], v[198:199], -%[m]\n\tv_and_b32 v199, 0x7fffffff, v199\n\t" \
+    "v_add_f64 v[200:201], v[200:201], -%[m]\n\tv_and_b32 v201, 0x7fffffff, v201\n\t" \
+    "v_add_f64 v[202:203], v[202:203], -%[m]\n\tv_and_b32 v203, 0x7fffffff, v203\n\t" \
+    "v_add_f64 v[204:205], v[204:205], -%[m]\n\tv_and_b32 v205, 0x7fffffff, v205\n\t" \
+    "v_add_f64 v[206:207], v[206:207], -%[m]\n\tv_and_b32 v207, 0x7fffffff, v207\n\t" \
+    "v_add_f64 v[208:209], v[208:209], -%[m]\n\tv_and_b32 v209, 0x7fffffff, v209\n\t" \
+    "v_add_f64 v[210:211], v[210:211], -%[m]\n\tv_and_b32 v211, 0x7fffffff, v211\n\t" \
+    "v_add_f64 v[212:213], v[212:213], -%[m]\n\tv_and_b32 v213, 0x7fffffff, v213\n\t" \
+    "v_add_f64 v[214:215], v[214:215], -%[m]\n\tv_and_b32 v215, 0x7fffffff, v215\n\t" \
+    "v_add_f64 v[216:217], v[216:217], -%[m]\n\tv_and_b32 v217, 0x7fffffff, v217\n\t" \
+    "v_add_f64 v[218:219], v[218:219], -%[m]\n\tv_and_b32 v219, 0x7fffffff, v219\n\t" \
+    "v_add_f64 v[220:221], v[220:221], -%[m]\n\tv_and_b32 v221, 0x7fffffff, v221\n\t" \
+    "v_add_f64 v[222:223], v[222:223], -%[m]\n\tv_and_b32 v223, 0x7fffffff, v223\n\t" \
+    "v_add_f64 v[224:225], v[224:225], -%[m]\n\tv_and_b32 v225, 0x7fffffff, v225\n\t" \
+    "v_add_f64 v[226:227], v[226:227], -%[m]\n\tv_and_b32 v227, 0x7fffffff, v227\n\t" \
+    "v_add_f64 v[228:229], v[228:229], -%[m]\n\tv_and_b32 v229, 0x7fffffff, v229\n\t" \
+    "v_add_f64 v[230:231], v[230:231], -%[m]\n\tv_and_b32 v231, 0x7fffffff, v231\n\t" \
+    "v_add_f64 v[232:233], v[232:233], -%[m]\n\tv_and_b32 v233, 0x7fffffff, v233\n\t" \
+    "v_add_f64 v[234:235], v[234:235], -%[m]\n\tv_and_b32 v235, 0x7fffffff, v235\n\t" \
+    "v_add_f64 v[236:237], v[236:237], -%[m]\n\tv_and_b32 v237, 0x7fffffff, v237\n\t" \
+    "v_add_f64 v[238:239], v[238:239], -%[m]\n\tv_and_b32 v239, 0x7fffffff, v239\n\t" \
+    "v_add_f64 v[240:241], v[240:241], -%[m]\n\tv_and_b32 v241, 0x7fffffff, v241\n\t" \
+    "v_add_f64 v[242:243], v[242:243], -%[m]\n\tv_and_b32 v243, 0x7fffffff, v243\n\t" \
+    "v_add_f64 v[244:245], v[244:245], -%[m]\n\tv_and_b32 v245, 0x7fffffff, v245\n\t" \
+    "v_add_f64 v[246:247], v[246:247], -%[m]\n\tv_and_b32 v247, 0x7fffffff, v247\n\t" \
+    "v_add_f64 v[248:249], v[248:249], -%[m]\n\tv_and_b32 v249, 0x7fffffff, v249\n\t" \
+    "v_add_f64 v[250:251], v[250:251], -%[m]\n\tv_and_b32 v251, 0x7fffffff, v251\n\t" \
+    "v_add_f64 v[252:253], v[252:253], -%[m]\n\tv_and_b32 v253, 0x7fffffff, v253\n\t" \
+    "v_add_f64 v[254:255], v[254:255], -%[m]\n\tv_and_b32 v255, 0x7fffffff, v255\n\t"
+
 // the lane's value in block-uniform row r / store x there.  Index mode writes M0; M0 is reserved to the
 // compiler, which uses it nowhere in these kernels (checked with the fence).  Volatile asm keeps the row
 // accesses in program order.
@@ -412,7 +504,10 @@ struct VSel {
     __device__ __forceinline__ void load(const double* src, bool mad, double med, bool preloaded) {
         if (!preloaded) load_raw(src);
         if (mad) {  // src/algorithm.cpp:860-863 (DBL_MAX stays DBL_MAX)
-            rows<true>(0, R - 1, [&](int, double& x) __attribute__((always_inline)) { x = fabs(x - med); });
+            const uint64_t mb = uni(__builtin_bit_cast(uint64_t, med));
+            asm volatile(SVO_VMAD_ASM ::[m] "s"(mb)
+                         : "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v164", "v165", "v166", "v167", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255");
+            rows<true>(kVRegRows, R - 1, [&](int, double& x) __attribute__((always_inline)) { x = fabs(x - med); });
         }
     }
     // this wave's rows r whose step 8 r + wave lies in [s0, s1] (rlo > rhi: none)

@@ -16,6 +16,8 @@ KERNELS = ("align_scale_refv_kernel", "debug_robust_scale_v_kernel")
 REG = re.compile(r"\bv\[?(\d+)(?::(\d+))?\]?")
 # the indexed data operands the asm blocks name (rows r..r+3 of an index session)
 DATA_OPERANDS = {f"v{i}" for i in range(80, 88)} | {f"v[{i}:{i + 1}]" for i in range(80, 88, 2)}
+# the fixed data operands of the MAD pass's in-place |x - med| block (every row's pair and its high word)
+MAD_OPERANDS = {f"v[{i}:{i + 1}]" for i in range(80, 256, 2)} | {f"v{i}" for i in range(81, 256, 2)}
 
 
 def check(path, fence=80):
@@ -46,10 +48,12 @@ def check(path, fence=80):
             ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
             for j, o in enumerate(ops):
                 # inside the asm blocks the data registers appear only as the indexed operands of the row
-                # moves / compares / selects (v80, v81, v[80:81]) and as the destinations of the row loads;
+                # moves / compares / selects (v80, v81, v[80:81]), as the destinations of the row loads and as
+                # the fixed rows of the MAD transform;
                 # every other operand is the compiler's and must stay below the fence
                 if in_asm and ((code.startswith(("v_mov_b32", "v_cndmask_b32", "v_cmp_")) and o in DATA_OPERANDS) or
-                               (code.startswith("buffer_load_dwordx2") and j == 0)):
+                               (code.startswith("buffer_load_dwordx2") and j == 0) or
+                               (code.startswith(("v_add_f64", "v_and_b32")) and o in MAD_OPERANDS)):
                     continue
                 for m in REG.finditer(o):
                     hi = int(m.group(2) or m.group(1))
