@@ -52,6 +52,10 @@ constexpr uint32_t kMbCap = 12288;    // mailbox (doubles); Ks beyond it exchang
 #endif
 constexpr uint32_t kOneWave = SVO_ONEWAVE;  // segments of <= kOneWave positions continue on wave 0
 static_assert(kOneWave % 64 == 0 && kOneWave / 64 <= kVRegRows && 2 * kOneWave <= kMbCap, "one-wave segment rows");
+// wave 0's register rows for the MAD pass, staged by the other waves during its one-wave rounds, past the one-wave
+// segment and its mailbox
+constexpr uint32_t kStage = 2 * kOneWave;
+static_assert(kStage + 64 * kVRegRows <= kMbCap, "staging of wave 0's rows inside the mailbox");
 #if defined(SVO_STAMPS)
 constexpr int kScanGroup = 2;         // record reads the scan keeps in flight (the stamps cost registers)
 #else
@@ -297,6 +301,98 @@ struct VDiag {  // svo_debug_robust_scale diagnostics
     "v_add_f64 v[252:253], v[252:253], -%[m]\n\tv_and_b32 v253, 0x7fffffff, v253\n\t" \
     "v_add_f64 v[254:255], v[254:255], -%[m]\n\tv_and_b32 v255, 0x7fffffff, v255\n\t"
 
+// wave 0's rows for the MAD pass from their LDS staging (stg[64 r + lane], byte offset 512 r from the lane's
+// address) straight into the data registers
+#define SVO_VLDS_ASM \
+    "ds_read_b64 v[80:81], %[a] offset:0\n\t" \
+    "ds_read_b64 v[82:83], %[a] offset:512\n\t" \
+    "ds_read_b64 v[84:85], %[a] offset:1024\n\t" \
+    "ds_read_b64 v[86:87], %[a] offset:1536\n\t" \
+    "ds_read_b64 v[88:89], %[a] offset:2048\n\t" \
+    "ds_read_b64 v[90:91], %[a] offset:2560\n\t" \
+    "ds_read_b64 v[92:93], %[a] offset:3072\n\t" \
+    "ds_read_b64 v[94:95], %[a] offset:3584\n\t" \
+    "ds_read_b64 v[96:97], %[a] offset:4096\n\t" \
+    "ds_read_b64 v[98:99], %[a] offset:4608\n\t" \
+    "ds_read_b64 v[100:101], %[a] offset:5120\n\t" \
+    "ds_read_b64 v[102:103], %[a] offset:5632\n\t" \
+    "ds_read_b64 v[104:105], %[a] offset:6144\n\t" \
+    "ds_read_b64 v[106:107], %[a] offset:6656\n\t" \
+    "ds_read_b64 v[108:109], %[a] offset:7168\n\t" \
+    "ds_read_b64 v[110:111], %[a] offset:7680\n\t" \
+    "ds_read_b64 v[112:113], %[a] offset:8192\n\t" \
+    "ds_read_b64 v[114:115], %[a] offset:8704\n\t" \
+    "ds_read_b64 v[116:117], %[a] offset:9216\n\t" \
+    "ds_read_b64 v[118:119], %[a] offset:9728\n\t" \
+    "ds_read_b64 v[120:121], %[a] offset:10240\n\t" \
+    "ds_read_b64 v[122:123], %[a] offset:10752\n\t" \
+    "ds_read_b64 v[124:125], %[a] offset:11264\n\t" \
+    "ds_read_b64 v[126:127], %[a] offset:11776\n\t" \
+    "ds_read_b64 v[128:129], %[a] offset:12288\n\t" \
+    "ds_read_b64 v[130:131], %[a] offset:12800\n\t" \
+    "ds_read_b64 v[132:133], %[a] offset:13312\n\t" \
+    "ds_read_b64 v[134:135], %[a] offset:13824\n\t" \
+    "ds_read_b64 v[136:137], %[a] offset:14336\n\t" \
+    "ds_read_b64 v[138:139], %[a] offset:14848\n\t" \
+    "ds_read_b64 v[140:141], %[a] offset:15360\n\t" \
+    "ds_read_b64 v[142:143], %[a] offset:15872\n\t" \
+    "ds_read_b64 v[144:145], %[a] offset:16384\n\t" \
+    "ds_read_b64 v[146:147], %[a] offset:16896\n\t" \
+    "ds_read_b64 v[148:149], %[a] offset:17408\n\t" \
+    "ds_read_b64 v[150:151], %[a] offset:17920\n\t" \
+    "ds_read_b64 v[152:153], %[a] offset:18432\n\t" \
+    "ds_read_b64 v[154:155], %[a] offset:18944\n\t" \
+    "ds_read_b64 v[156:157], %[a] offset:19456\n\t" \
+    "ds_read_b64 v[158:159], %[a] offset:19968\n\t" \
+    "ds_read_b64 v[160:161], %[a] offset:20480\n\t" \
+    "ds_read_b64 v[162:163], %[a] offset:20992\n\t" \
+    "ds_read_b64 v[164:165], %[a] offset:21504\n\t" \
+    "ds_read_b64 v[166:167], %[a] offset:22016\n\t" \
+    "ds_read_b64 v[168:169], %[a] offset:22528\n\t" \
+    "ds_read_b64 v[170:171], %[a] offset:23040\n\t" \
+    "ds_read_b64 v[172:173], %[a] offset:23552\n\t" \
+    "ds_read_b64 v[174:175], %[a] offset:24064\n\t" \
+    "ds_read_b64 v[176:177], %[a] offset:24576\n\t" \
+    "ds_read_b64 v[178:179], %[a] offset:25088\n\t" \
+    "ds_read_b64 v[180:181], %[a] offset:25600\n\t" \
+    "ds_read_b64 v[182:183], %[a] offset:26112\n\t" \
+    "ds_read_b64 v[184:185], %[a] offset:26624\n\t" \
+    "ds_read_b64 v[186:187], %[a] offset:27136\n\t" \
+    "ds_read_b64 v[188:189], %[a] offset:27648\n\t" \
+    "ds_read_b64 v[190:191], %[a] offset:28160\n\t" \
+    "ds_read_b64 v[192:193], %[a] offset:28672\n\t" \
+    "ds_read_b64 v[194:195], %[a] offset:29184\n\t" \
+    "ds_read_b64 v[196:197], %[a] offset:29696\n\t" \
+    "ds_read_b64 v[198:199], %[a] offset:30208\n\t" \
+    "ds_read_b64 v[200:201], %[a] offset:30720\n\t" \
+    "ds_read_b64 v[202:203], %[a] offset:31232\n\t" \
+    "ds_read_b64 v[204:205], %[a] offset:31744\n\t" \
+    "ds_read_b64 v[206:207], %[a] offset:32256\n\t" \
+    "ds_read_b64 v[208:209], %[a] offset:32768\n\t" \
+    "ds_read_b64 v[210:211], %[a] offset:33280\n\t" \
+    "ds_read_b64 v[212:213], %[a] offset:33792\n\t" \
+    "ds_read_b64 v[214:215], %[a] offset:34304\n\t" \
+    "ds_read_b64 v[216:217], %[a] offset:34816\n\t" \
+    "ds_read_b64 v[218:219], %[a] offset:35328\n\t" \
+    "ds_read_b64 v[220:221], %[a] offset:35840\n\t" \
+    "ds_read_b64 v[222:223], %[a] offset:36352\n\t" \
+    "ds_read_b64 v[224:225], %[a] offset:36864\n\t" \
+    "ds_read_b64 v[226:227], %[a] offset:37376\n\t" \
+    "ds_read_b64 v[228:229], %[a] offset:37888\n\t" \
+    "ds_read_b64 v[230:231], %[a] offset:38400\n\t" \
+    "ds_read_b64 v[232:233], %[a] offset:38912\n\t" \
+    "ds_read_b64 v[234:235], %[a] offset:39424\n\t" \
+    "ds_read_b64 v[236:237], %[a] offset:39936\n\t" \
+    "ds_read_b64 v[238:239], %[a] offset:40448\n\t" \
+    "ds_read_b64 v[240:241], %[a] offset:40960\n\t" \
+    "ds_read_b64 v[242:243], %[a] offset:41472\n\t" \
+    "ds_read_b64 v[244:245], %[a] offset:41984\n\t" \
+    "ds_read_b64 v[246:247], %[a] offset:42496\n\t" \
+    "ds_read_b64 v[248:249], %[a] offset:43008\n\t" \
+    "ds_read_b64 v[250:251], %[a] offset:43520\n\t" \
+    "ds_read_b64 v[252:253], %[a] offset:44032\n\t" \
+    "ds_read_b64 v[254:255], %[a] offset:44544\n\t"
+
 // the lane's value in block-uniform row r / store x there.  Index mode writes M0; M0 is reserved to the
 // compiler, which uses it nowhere in these kernels (checked with the fence).  Volatile asm keeps the row
 // accesses in program order.
@@ -499,6 +595,27 @@ struct VSel {
             const uint32_t q = (uint32_t)r * kVT + (uint32_t)tid;
             sh.lrow[r - kVRegRows][tid] = q < M ? src[q] : 0.0;
         }
+    }
+    // waves 1..7, during wave 0's one-wave rounds: wave 0's rows of src into LDS, the register rows to
+    // mbx[kStage + 64 r + lane] (wave 0 moves them into its registers after the pass's last barrier: an LDS
+    // latency instead of a memory latency on the critical path), the LDS rows straight into wave 0's lrow entries
+    __device__ __forceinline__ void stage_wave0(const double* src) {
+        double* const stg = sh.mbx + kStage;
+#pragma unroll
+        for (int i = 0; i < R / (kVW - 1); ++i) {
+            const int r = wave - 1 + (kVW - 1) * i;
+            const uint32_t q = (uint32_t)r * kVT + (uint32_t)lane;
+            const double x = q < M ? src[q] : 0.0;
+            if (r < kVRegRows) stg[64 * r + lane] = x;
+            else sh.lrow[r - kVRegRows][lane] = x;
+        }
+    }
+    __device__ __forceinline__ void unstage_wave0() {
+        const uint32_t a = (uint32_t)(uintptr_t)(sh.mbx + kStage) + 8u * (uint32_t)lane;
+        asm volatile(SVO_VLDS_ASM "s_waitcnt lgkmcnt(0)"
+                     :
+                     : [a] "v"(a)
+                     : "memory", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159", "v160", "v161", "v162", "v163", "v164", "v165", "v166", "v167", "v168", "v169", "v170", "v171", "v172", "v173", "v174", "v175", "v176", "v177", "v178", "v179", "v180", "v181", "v182", "v183", "v184", "v185", "v186", "v187", "v188", "v189", "v190", "v191", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202", "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213", "v214", "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238", "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250", "v251", "v252", "v253", "v254", "v255");
     }
     // preloaded: the rows were loaded already (the MAD pass's rows, during the median pass's one-wave rounds)
     __device__ __forceinline__ void load(const double* src, bool mad, double med, bool preloaded) {
@@ -1170,7 +1287,10 @@ struct VSel {
             dump(seg, f0, sh.mbx + kMbCap);
             __syncthreads();
             did_preload = preload_next;
-            if (preload_next && wave != 0) load_raw(src);
+            if (preload_next && wave != 0) {
+                load_raw(src);
+                stage_wave0(src);
+            }
             if (wave == 0) {
                 uint32_t nw = 0;
                 wave_rounds(seg, sh.mbx + kOneWave, nw);
@@ -1190,10 +1310,12 @@ struct VSel {
                     }
                     if (dg) dg->nwave[P] = nw;
                 }
-                if (preload_next) load_raw(src);  // (after the rounds: they used only LDS)
             }
         }
         __syncthreads();  // seg / mailbox / gseg are reused by the next pass
+        // wave 0's staged rows (the next pass writes the mailbox only after its first barrier, which wave 0
+        // reaches after these reads have completed)
+        if (did_preload && wave == 0) unstage_wave0();
         VSTAMP(7);
         if (dg && tid == 0) {
             dg->nblock[P] = nblock;

@@ -16,7 +16,8 @@ KERNELS = ("align_scale_refv_kernel", "debug_robust_scale_v_kernel")
 REG = re.compile(r"\bv\[?(\d+)(?::(\d+))?\]?")
 # the indexed data operands the asm blocks name (rows r..r+3 of an index session)
 DATA_OPERANDS = {f"v{i}" for i in range(80, 88)} | {f"v[{i}:{i + 1}]" for i in range(80, 88, 2)}
-# the fixed data operands of the MAD pass's in-place |x - med| block (every row's pair and its high word)
+# the fixed data operands of the MAD pass's in-place |x - med| block (every row's pair and its high word) and of
+# the LDS reads of wave 0's staged rows
 MAD_OPERANDS = {f"v[{i}:{i + 1}]" for i in range(80, 256, 2)} | {f"v{i}" for i in range(81, 256, 2)}
 
 
@@ -53,7 +54,8 @@ def check(path, fence=80):
                 # every other operand is the compiler's and must stay below the fence
                 if in_asm and ((code.startswith(("v_mov_b32", "v_cndmask_b32", "v_cmp_")) and o in DATA_OPERANDS) or
                                (code.startswith("buffer_load_dwordx2") and j == 0) or
-                               (code.startswith(("v_add_f64", "v_and_b32")) and o in MAD_OPERANDS)):
+                               (code.startswith(("v_add_f64", "v_and_b32")) and o in MAD_OPERANDS) or
+                               (code.startswith("ds_read_b64") and j == 0 and o in MAD_OPERANDS)):
                     continue
                 for m in REG.finditer(o):
                     hi = int(m.group(2) or m.group(1))
