@@ -46,7 +46,14 @@ def parse():
     ap.add_argument("--features", type=int, default=2000)
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--patch", type=int, default=5)
-    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic scenes per rank")
+    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic scenes per scene block")
+    ap.add_argument("--scene-block", type=int, default=0,
+                    help="global pair g uses the scene seeded SEED_BASE + (g // B) * B + (g % B) %% distinct, B = this "
+                         "value (default: --pairs, i.e. each rank's own block): the job's pairs are then the same "
+                         "whatever the number of ranks, e.g. --gpus 2 --pairs P and --gpus 1 --pairs 2P --scene-block P")
+    ap.add_argument("--dump-poses", default="",
+                    help="rank 0 writes every rank's per-pair seeds, poses, errors and statuses (gathered in rank order) "
+                         "to this .npz (G-invariance tests)")
     ap.add_argument("--feature-order", choices=("cell", "shuffled"), default="cell",
                     help="cell: features in the order the reference detector emits them (30-px grid cells row by "
                          "row, src/feature_selection.cpp:103-141); shuffled: random order")
@@ -84,14 +91,32 @@ def level_bytes(w, h, levels):
     return tot
 
 
-def packed_pairs(scenes, P, D):
-    """svo_align_batch_set_pairs inputs for pairs 0..P-1 (pair i = scene i % D, frames 3i .. 3i+2)."""
+def packed_pairs(scenes, P, D, idx=None):
+    """svo_align_batch_set_pairs inputs for pairs 0..P-1 (pair i = scene idx[i], default i % D; frames 3i .. 3i+2)."""
+    idx = [i % D for i in range(P)] if idx is None else idx
     frames = np.arange(3 * P, dtype=np.int32).reshape(P, 3)
-    poses = np.stack([np.concatenate([scenes[i % D].ref_pose, scenes[i % D].kf_pose, scenes[i % D].cur_init_pose])
+    poses = np.stack([np.concatenate([scenes[idx[i]].ref_pose, scenes[idx[i]].kf_pose, scenes[idx[i]].cur_init_pose])
                       for i in range(P)])
-    n_feat = np.array([[scenes[i % D].n_ref, scenes[i % D].n_kf] for i in range(P)], np.int32)
-    cat = lambda f: np.ascontiguousarray(np.concatenate([getattr(scenes[i % D], f) for i in range(P)]))
+    n_feat = np.array([[scenes[idx[i]].n_ref, scenes[idx[i]].n_kf] for i in range(P)], np.int32)
+    cat = lambda f: np.ascontiguousarray(np.concatenate([getattr(scenes[idx[i]], f) for i in range(P)]))
     return frames, poses, n_feat, cat("px"), cat("bearing"), cat("point"), cat("has_point").astype(np.uint8)
+
+
+def scene_seeds(first, count, block, distinct):
+    """Seed of each global pair g in [first, first + count): SEED_BASE + (g // block) * block + (g % block) % distinct."""
+    return [synth.SEED_BASE + (g // block) * block + (g % block) % distinct for g in range(first, first + count)]
+
+
+def image_chunks(scenes, idx, chunk):
+    """Base images of pairs [c, c + chunk) as (first pair, (3 * count, H, W) array) per chunk; chunks with the same
+    scenes share one array (the default mapping repeats every `distinct` pairs, so there is one)."""
+    out, cache = [], {}
+    for c in range(0, len(idx), chunk):
+        key = tuple(idx[c:c + chunk])
+        if key not in cache:
+            cache[key] = np.stack([im for k in key for im in (scenes[k].ref_img, scenes[k].kf_img, scenes[k].cur_img)])
+        out.append((c, cache[key]))
+    return out
 
 
 def canon(p):
@@ -149,17 +174,20 @@ def main():
     nthreads = max(1, min(16, os.cpu_count() or 1))
     first, _ = shard.pair_block(world * P, rank, world)  # this rank's block of the job's world * P pairs
     cell = 30 if args.feature_order == "cell" else 0  # config "cell_pixel_size": 30
-    scenes = [synth.make_pair(seed=synth.SEED_BASE + first + i, n_features=nf, patch_size=patch, nthreads=nthreads,
-                              cell_order=cell) for i in range(D)]
+    seeds = scene_seeds(first, P, args.scene_block or P, D)
+    useeds = sorted(set(seeds))
+    sidx = [useeds.index(s) for s in seeds]  # pair j -> its scene in `scenes`
+    scenes = [synth.make_pair(seed=sd, n_features=nf, patch_size=patch, nthreads=nthreads, cell_order=cell)
+              for sd in useeds]
     cam = scenes[0].camera
     camera = svo_amd.PinholeCamera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"])
+    rep = [sidx.index(k) for k in range(len(scenes))]  # the first pair of each scene
 
     # device-resident inputs: 3 pyramids per pair, each pair in its own buffers
     ps = svo_amd.PyramidSet(3 * P, cam["width"], cam["height"], L, ctx)
-    base = np.stack([im for s in scenes for im in (s.ref_img, s.kf_img, s.cur_img)])
-    for first in range(0, P, D):
-        cnt = min(D, P - first)
-        ps.upload(3 * first, base[:3 * cnt])
+    chunks = image_chunks(scenes, sidx, D)
+    for c, arr in chunks:
+        ps.upload(3 * c, arr)
     ctx.synchronize()
     ps.build()  # warm-up (the first launch loads the code objects)
     pyr_runs = []
@@ -174,7 +202,7 @@ def main():
 
     mode = svo_amd.MEDIAN_REFERENCE if args.median == "reference" else svo_amd.MEDIAN_EXACT
     batch = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx, median_mode=mode)
-    packed = packed_pairs(scenes, P, D)  # the caller's feature arrays (built outside every timed region)
+    packed = packed_pairs(scenes, P, D, sidx)  # the caller's feature arrays (built outside every timed region)
     batch.set_pairs(0, ps, ps, ps, *packed)
 
     for _ in range(args.warmup):
@@ -201,7 +229,18 @@ def main():
 
     poses, err, status = batch.results()
     # every pair repeats its scene's pose bit for bit (pairs i and i + 256 run in different half-batch chains)
-    poses_repeat = bool(all(np.array_equal(poses[i], poses[i % D]) and err[i] == err[i % D] for i in range(P)))
+    poses_repeat = bool(all(np.array_equal(poses[i], poses[rep[sidx[i]]]) and err[i] == err[rep[sidx[i]]]
+                            for i in range(P)))
+    if args.dump_poses:  # every rank's per-pair results, gathered in rank order (host side, outside the timing)
+        mine = (np.array(seeds, np.int64), poses, err, status)
+        parts = [mine]
+        if dist:
+            parts = [None] * world
+            dist.all_gather_object(parts, mine)
+        if rank == 0:
+            np.savez(args.dump_poses, seeds=np.concatenate([q[0] for q in parts]),
+                     poses=np.concatenate([q[1] for q in parts]), err=np.concatenate([q[2] for q in parts]),
+                     status=np.concatenate([q[3] for q in parts]), world=world)
     # per-step time: median of 20 single synchronized steps (host clock), after the timed region
     step_s = []
     for _ in range(20):
@@ -216,9 +255,8 @@ def main():
     # build the pyramids, hand over every pair's features and poses, align, read the results back
     ctx.synchronize()
     e2e_t0 = time.perf_counter()
-    for first in range(0, P, D):
-        cnt = min(D, P - first)
-        ps.upload(3 * first, base[:3 * cnt])
+    for c, arr in chunks:
+        ps.upload(3 * c, arr)
     ps.build()
     batch.set_pairs(0, ps, ps, ps, *packed)
     batch.run()
@@ -237,6 +275,32 @@ def main():
         batch.results()
         e2d_runs.append(time.perf_counter() - e2d_t0)
     e2d_s = float(np.median(e2d_runs))
+    # the same hand-over for a stream of batches (a tracker's steady state): batch i + 1's pyramids build on the
+    # context's prep stream (a second PyramidSet) while batch i's features are handed over and it aligns
+    # (src/frame.cpp:26 builds each frame's pyramid before the frame is aligned); per batch: one build, one
+    # set_pairs, one alignment, one read-back
+    e2p_ms = None
+    if not args.core_only:
+        ps2 = svo_amd.PyramidSet(3 * P, cam["width"], cam["height"], L, ctx)
+        for c, arr in chunks:
+            ps2.upload(3 * c, arr)
+        sets = (ps, ps2)
+        ps.build()
+        ctx.synchronize()
+        K = 8
+        e2p_t0 = time.perf_counter()
+        for i in range(K):
+            cur_set, nxt = sets[i % 2], sets[(i + 1) % 2]
+            nxt.build_async()
+            batch.set_pairs(0, cur_set, cur_set, cur_set, *packed)
+            batch.run()
+            pk, _, _ = batch.results()
+            if not np.array_equal(pk, poses):
+                raise SystemExit("bench.py: pipelined end-to-end poses differ from the timed run")
+        e2p_ms = (time.perf_counter() - e2p_t0) / K * 1e3
+        ctx.synchronize()
+        batch.set_pairs(0, ps, ps, ps, *packed)  # (back on the first set)
+        del ps2
     # the other median semantics on the same pairs: its rate and how far its poses are from the reference's
     other = svo_amd.MEDIAN_EXACT if mode == svo_amd.MEDIAN_REFERENCE else svo_amd.MEDIAN_REFERENCE
     other_line, lat = None, None
@@ -317,17 +381,22 @@ def main():
         "end_to_end": {"pairs": P, "ms": round(e2e_s * 1e3, 3), "pairs_per_s": round(P / e2e_s, 1),
                        "note": "from host memory: H2D of 3P base images (pageable), pyramid build, all pairs' "
                                "features / poses in one svo_align_batch_set_pairs call, alignment, D2H of the results"},
-        "end_to_end_device_images": {"pairs": P, "ms": round(e2d_s * 1e3, 3), "pairs_per_s": round(P / e2d_s, 1),
-                                     "runs": 5, "statistic": "median",
-                                     "note": "SURVEY 8(d): base images already in HBM; pyramid build, all pairs' "
-                                             "features / poses from host memory in one svo_align_batch_set_pairs "
-                                             "call, alignment, D2H of the results"},
+        "end_to_end_device_images": None if e2p_ms is None else {
+            "pairs": P, "ms": round(e2p_ms, 3), "pairs_per_s": round(P / (e2p_ms * 1e-3), 1), "batches": 8,
+            "statistic": "mean over a stream of 8 batches",
+            "note": "SURVEY 8(d): base images already in HBM; per batch a pyramid build, all pairs' features / poses "
+                    "from host memory in one svo_align_batch_set_pairs call, alignment, D2H of the results; batch i+1's "
+                    "pyramids build (svo_pyramid_set_build_async, a second PyramidSet) while batch i aligns"},
+        "end_to_end_device_images_single": {"pairs": P, "ms": round(e2d_s * 1e3, 3), "pairs_per_s": round(P / e2d_s, 1),
+                                            "runs": 5, "statistic": "median",
+                                            "note": "one batch at a time: pyramid build, set_pairs, alignment, D2H, "
+                                                    "nothing overlapped"},
         "latency": lat,
     }
     if not args.no_secondary:
         out["secondary"] = secondary(args, ctx, scenes[0], cam, camera)
     if not args.no_cpu and world == 1:
-        out.update(cpu_baseline(args, scenes, poses, L, patch, nthreads, mode))
+        out.update(cpu_baseline(args, scenes, poses[rep], L, patch, nthreads, mode))
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
@@ -652,12 +721,29 @@ def secondary(args, ctx, scene, cam, camera, reps=20):
     return res
 
 
+def physical_cores():
+    """Physical cores of this host (sockets x "cpu cores" in /proc/cpuinfo), or None."""
+    try:
+        socks, cores = set(), None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    socks.add(line.split(":", 1)[1].strip())
+                elif line.startswith("cpu cores") and cores is None:
+                    cores = int(line.split(":", 1)[1])
+        return len(socks or {"0"}) * cores if cores else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(args, scenes, gpu_poses, L, patch, nthreads, mode=None):
-    """The oracle (faithful C++ restatement, -O3) timed on this host on a bounded sample of the same
-    workload: one thread, and one pinned thread per available CPU (the process affinity
-    mask, capped by the box's CPU share OMP_NUM_THREADS); each the median of 20 runs after 3 warm-ups.
-    Also the SE(3) error of the GPU poses against the oracle on every distinct scene (the bench checks that
-    all pairs repeat their scene's pose bit for bit, so this covers both half-batch chains)."""
+    """The oracle (faithful C++ restatement) timed on this host on a bounded sample of the same workload
+    (SURVEY 8(d)(ii)), in two builds: the CPU-baseline build made here at bench time with BASELINE.md's Release
+    flags (-O3 -DNDEBUG -march=native, FMA contraction allowed: oracle/Makefile `native`) and the portable parity
+    build (-march=x86-64-v3 -ffp-contract=off, the checker).  One thread, and one pinned thread per available CPU
+    (the process affinity mask, capped by the box's CPU share OMP_NUM_THREADS); each the median of 20 runs after
+    3 warm-ups.  Also the SE(3) error of the GPU poses against the parity oracle on every distinct scene (the bench
+    checks that all pairs repeat their scene's pose bit for bit, so this covers both half-batch chains)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # noqa: E402  (CPU baseline / checker only)
     omode = 1 if mode == svo_amd.MEDIAN_EXACT else 0  # oracle median_mode 0 = the reference's nth_element
@@ -668,16 +754,6 @@ def cpu_baseline(args, scenes, gpu_poses, L, patch, nthreads, mode=None):
     for i, s in enumerate(scenes):
         pose, _, _, _ = O.image_align(s.camera, patch, 0, L - 1, pairs[i], s.cur_init_pose, omode)
         se3_err = max(se3_err, float(np.abs(canon(pose) - canon(gpu_poses[i])).max()))
-    # one thread: 3 warm-ups, 20 timed alignments
-    ts = []
-    for r in range(23):
-        i = r % len(scenes)
-        t = time.perf_counter()
-        O.image_align(scenes[i].camera, patch, 0, L - 1, pairs[i], scenes[i].cur_init_pose, omode)
-        if r >= 3:
-            ts.append(time.perf_counter() - t)
-    single = 1.0 / float(np.median(ts))
-    # all available CPUs, one pinned worker each: runs of 2 alignments per thread
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     share = int(os.environ.get("OMP_NUM_THREADS", avail) or avail)
     threads = max(1, min(avail, share))
@@ -685,22 +761,59 @@ def cpu_baseline(args, scenes, gpu_poses, L, patch, nthreads, mode=None):
     idx = [i % len(scenes) for i in range(n_mt)]
     sel = [pairs[i] for i in idx]
     init = np.stack([scenes[i].cur_init_pose for i in idx])
-    rates = []
-    for r in range(23):
-        t = time.perf_counter()
-        O.image_align_batch(scenes[0].camera, patch, 0, L - 1, sel, init, omode, threads)
-        if r >= 3:
-            rates.append(n_mt / (time.perf_counter() - t))
-    multi = float(np.median(rates))
+
+    def timed(Lib):
+        ts = []  # one thread: 3 warm-ups, 20 timed alignments
+        for r in range(23):
+            i = r % len(scenes)
+            t = time.perf_counter()
+            O.image_align(scenes[i].camera, patch, 0, L - 1, pairs[i], scenes[i].cur_init_pose, omode, L=Lib)
+            if r >= 3:
+                ts.append(time.perf_counter() - t)
+        rates = []  # all available CPUs, one pinned worker each: runs of 2 alignments per thread
+        for r in range(23):
+            t = time.perf_counter()
+            O.image_align_batch(scenes[0].camera, patch, 0, L - 1, sel, init, omode, threads, L=Lib)
+            if r >= 3:
+                rates.append(n_mt / (time.perf_counter() - t))
+        return 1.0 / float(np.median(ts)), float(np.median(rates))
+
+    port_single, port_multi = timed(None)
+    nat = O.native_lib()
+    nat_single = nat_multi = None
+    nat_diff = None
+    if nat is not None:
+        nat_single, nat_multi = timed(nat)
+        nat_diff = max(float(np.abs(canon(O.image_align(s.camera, patch, 0, L - 1, pairs[i], s.cur_init_pose, omode,
+                                                           L=nat)[0])
+                                    - canon(O.image_align(s.camera, patch, 0, L - 1, pairs[i], s.cur_init_pose,
+                                                          omode)[0])).max())
+                       for i, s in enumerate(scenes))
+    single, multi = (nat_single, nat_multi) if nat is not None else (port_single, port_multi)
+    build = ("oracle/svo_oracle.cpp, -O3 -DNDEBUG -march=native (built on this host at bench time, FMA contraction "
+             "allowed)" if nat is not None else
+             "oracle/svo_oracle.cpp, -O3 -DNDEBUG -march=x86-64-v3 -ffp-contract=off (the native build failed)")
+    phys = physical_cores()
     return {
         "cpu_baseline": {"value": round(single, 3), "unit": "pairs/s", "cores": 1, "kind": "port",
-                         "cpu_model": cpu_model(),
+                         "cpu_model": cpu_model(), "build": build,
                          "sample": "median of 20 single ImageAlignment::align calls (config 2 shape, "
-                                   f"{len(scenes)} scenes) after 3 warm-ups, 1 host thread, oracle/svo_oracle.cpp -O3"},
+                                   f"{len(scenes)} scenes) after 3 warm-ups, 1 host thread"},
         "cpu_baseline_multicore": {"value": round(multi, 3), "unit": "pairs/s", "cores": threads, "kind": "port",
-                                   "available_cpus": avail, "cpu_share": share,
+                                   "available_cpus": avail, "cpu_share": share, "build": build,
                                    "sample": f"median of 20 runs of {n_mt} alignments ({threads} threads pinned one per "
-                                             "available CPU, one alignment per thread at a time) after 3 warm-ups"},
+                                             "available CPU, one alignment per thread at a time) after 3 warm-ups",
+                                   "physical_cores_of_host": phys,
+                                   "extrapolated_full_host_pairs_per_s": (round(single * phys, 1) if phys else None),
+                                   "extrapolation_note": "1-thread rate x the host's physical cores (linear, no memory "
+                                                         "or clock effects): the rate the whole host would give if every "
+                                                         "core ran one alignment; this box grants the process only "
+                                                         "cpu_share CPUs"},
+        "cpu_baseline_portable_build": {"value": round(port_single, 3), "multicore_value": round(port_multi, 3),
+                                        "unit": "pairs/s",
+                                        "build": "oracle/svo_oracle.cpp, -O3 -DNDEBUG -march=x86-64-v3 -ffp-contract=off "
+                                                 "(the parity checker)",
+                                        "max_abs_pose_diff_native_vs_portable": nat_diff},
         "se3_err_vs_ref": {"max_abs_param_diff": se3_err, "pairs": len(scenes),
                            "reference_semantics": ("libstdc++ nth_element median (oracle median_mode 0)" if omode == 0
                                                    else "exact order statistics (oracle median_mode 1)")},

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SVO_ABI_VERSION 1
+#define SVO_ABI_VERSION 2
 
 enum {
     SVO_OK = 0,
@@ -86,6 +86,9 @@ typedef struct {
     int32_t level, n_ref_vis, n_vis, status;
     double median, mad, sigma, chi2, lambda, err;
     double H[36], g[6], dx[6];
+    int32_t scale_kernel; /* the device kernel that computed median / MAD at this level: SVO_SCALE_K2R,
+                             SVO_SCALE_K2V or SVO_SCALE_K2 (exact mode); 0 if the level did not run */
+    int32_t reserved;
 } svo_level_trace;
 
 /* ---------------------------------------------------------------- context */
@@ -117,6 +120,11 @@ int svo_pyramid_set_upload(svo_pyramid_set* set, int32_t first, int32_t count, c
 int svo_pyramid_set_upload_device(svo_pyramid_set* set, int32_t first, int32_t count, const uint8_t* dev_images);
 /* Build both stacks for frames [first, first+count) on the device.  Async (context stream). */
 int svo_pyramid_set_build(svo_pyramid_set* set, int32_t first, int32_t count);
+/* The same build on the context's prep stream, after everything queued on the context stream so far, so that it
+ * overlaps work queued later (the next batch's pyramids building while the current batch aligns:
+ * src/frame.cpp:26 -> src/image_pyramid.cpp:36-52 for the frames of the next call).  Every later use of the set's
+ * planes through this ABI (upload, build, download, svo_align_batch_set_pair / set_pairs) waits for it. */
+int svo_pyramid_set_build_async(svo_pyramid_set* set, int32_t first, int32_t count);
 /* ImagePyramid::getImageAtLevel / getGradientAtLevel (src/image_pyramid.cpp:54-124): copy one level
  * to the host (synchronous).  gradient = 0 for the intensity stack, 1 for the gradient stack. */
 int svo_pyramid_set_download(const svo_pyramid_set* set, int32_t frame, int32_t level, int32_t gradient, uint8_t* out);
@@ -182,7 +190,7 @@ int svo_align_batch_traces(svo_align_batch* batch, int32_t pair, svo_level_trace
 /* Device forms of the reference robust scale (SVO_MEDIAN_REFERENCE): K2V keeps the residual vector in
  * registers (vectors of <= 50 176 slots: config 2's 2000 features x 25), K2R runs its large rounds through
  * global scratch (any size).  Both give the same bits. */
-enum { SVO_SCALE_AUTO = 0, SVO_SCALE_K2R = 1, SVO_SCALE_K2V = 2 };
+enum { SVO_SCALE_AUTO = 0, SVO_SCALE_K2R = 1, SVO_SCALE_K2V = 2, SVO_SCALE_K2 = 3 /* exact mode (trace only) */ };
 
 /* Diagnostics (no reference counterpart): the SVO_MEDIAN_REFERENCE robust scale of an arbitrary residual
  * vector, i.e. algorithm::computeMAD(values, n_valid) (src/algorithm.cpp:855-865) and the median it uses, on
@@ -196,6 +204,9 @@ enum { SVO_SCALE_AUTO = 0, SVO_SCALE_K2R = 1, SVO_SCALE_K2V = 2 };
  * Synchronous.  SVO_ERR_ARG if impl is K2V and the vector does not fit it. */
 int svo_debug_robust_scale(svo_ctx* ctx, const double* values, int64_t n_slots, int64_t n_valid, int32_t impl,
                            double* out, int64_t out_len);
+/* The largest residual vector (slots = features x patch^2) the robust-scale kernel `impl` (SVO_SCALE_K2V or
+ * SVO_SCALE_K2R) takes.  A reference-mode launch runs K2V when every pair's vector fits it, K2R otherwise. */
+int svo_robust_scale_capacity(int32_t impl, int64_t* slots);
 
 /* ---------------------------------------------------------------- FeatureAlignment
  * Replaces FeatureAlignment::align(refFeature, curFrame, pixelPos) (src/feature_alignment.cpp:25-62,

@@ -46,6 +46,35 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+_NATIVE_PATH = os.path.join(_HERE, "build", "native", "libsvo_oracle.so")
+_native = None
+
+
+def native_lib(timeout=300):
+    """The same restatement built for this host's CPU (make native: -O3 -DNDEBUG -march=native, FMA contraction
+    allowed): the CPU BASELINE build (BASELINE.md's Release flags), built on first use.  Only bench.py's
+    cpu_baseline times it; the parity checker stays the contraction-free lib().  None if it cannot be built."""
+    global _native
+    if _native is None:
+        try:
+            subprocess.run(["make", "-s", "-C", _HERE, "native"], check=True, timeout=timeout,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+            _native = _load(_NATIVE_PATH)
+        except (OSError, subprocess.SubprocessError):
+            return None
+    return _native
+
+
+def _load(path):
+    L = ctypes.CDLL(path)
+    L.oracle_pyramid_bytes.restype = ctypes.c_int64
+    L.oracle_image_align.restype = ctypes.c_double
+    L.oracle_median.restype = ctypes.c_double
+    L.oracle_median.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int32]
+    assert L.oracle_level_trace_size() == ctypes.sizeof(LevelTrace)
+    return L
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -181,24 +210,25 @@ def make_pair(ref_pyr, kf_pyr, cur_pyr, ref_pose, kf_pose, n_ref, n_kf, px, bear
     return _PairKeep(P, keep + feats)
 
 
-def image_align(cam, patch, min_level, max_level, pair, cur_pose, median_mode=0, trace=False):
-    """ImageAlignment::align.  Returns (pose[7], err, status, traces or None)."""
+def image_align(cam, patch, min_level, max_level, pair, cur_pose, median_mode=0, trace=False, L=None):
+    """ImageAlignment::align.  Returns (pose[7], err, status, traces or None).  L: another build of the
+    oracle library (native_lib()), default lib()."""
     pose = np.ascontiguousarray(cur_pose, dtype=np.float64).copy()
     st = ctypes.c_int32()
     traces = (LevelTrace * (max_level + 1))() if trace else None
-    err = lib().oracle_image_align(ctypes.byref(camera(cam)), patch, min_level, max_level, median_mode,
+    err = (L or lib()).oracle_image_align(ctypes.byref(camera(cam)), patch, min_level, max_level, median_mode,
                                    ctypes.byref(pair.pair), _p(pose), ctypes.byref(st),
                                    ctypes.cast(traces, ctypes.c_void_p) if trace else None)
     return pose, err, st.value, traces
 
 
-def image_align_batch(cam, patch, min_level, max_level, pairs, cur_poses, median_mode=0, nthreads=1):
+def image_align_batch(cam, patch, min_level, max_level, pairs, cur_poses, median_mode=0, nthreads=1, L=None):
     n = len(pairs)
     arr = (OcPair * n)(*[p.pair for p in pairs])
     poses = np.ascontiguousarray(cur_poses, dtype=np.float64).copy()
     err = np.zeros(n)
     st = np.zeros(n, np.int32)
-    lib().oracle_image_align_batch(ctypes.byref(camera(cam)), patch, min_level, max_level, median_mode, n, arr,
+    (L or lib()).oracle_image_align_batch(ctypes.byref(camera(cam)), patch, min_level, max_level, median_mode, n, arr,
                                    _p(poses), _p(err), _p(st), nthreads)
     return poses, err, st
 

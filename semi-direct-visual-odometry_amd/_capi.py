@@ -42,7 +42,7 @@ class SvoLevelTrace(ctypes.Structure):
     _fields_ = [("level", c_int32), ("n_ref_vis", c_int32), ("n_vis", c_int32), ("status", c_int32),
                 ("median", c_double), ("mad", c_double), ("sigma", c_double), ("chi2", c_double),
                 ("lambda_", c_double), ("err", c_double), ("H", c_double * 36), ("g", c_double * 6),
-                ("dx", c_double * 6)]
+                ("dx", c_double * 6), ("scale_kernel", c_int32), ("reserved", c_int32)]
 
 
 # (name, restype, argtypes) for every entry point of include/svo_c.h
@@ -61,6 +61,7 @@ _SIGNATURES = [
     ("svo_pyramid_set_upload", c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     ("svo_pyramid_set_upload_device", c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     ("svo_pyramid_set_build", c_int32, [c_void_p, c_int32, c_int32]),
+    ("svo_pyramid_set_build_async", c_int32, [c_void_p, c_int32, c_int32]),
     ("svo_pyramid_set_download", c_int32, [c_void_p, c_int32, c_int32, c_int32, c_void_p]),
     ("svo_pyramid_level_size", c_int32, [c_void_p, c_int32, P_i32, P_i32]),
     ("svo_align_batch_create", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), ctypes.POINTER(SvoAlignParams),
@@ -76,6 +77,7 @@ _SIGNATURES = [
     ("svo_align_batch_profile", c_int32, [c_void_p, ctypes.POINTER(ctypes.c_float)]),
     ("svo_align_batch_results", c_int32, [c_void_p, c_void_p, c_void_p, c_void_p]),
     ("svo_align_batch_traces", c_int32, [c_void_p, c_int32, c_void_p]),
+    ("svo_robust_scale_capacity", c_int32, [c_int32, c_void_p]),
     ("svo_debug_robust_scale", c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, c_int32, c_void_p, ctypes.c_int64]),
     ("svo_feature_align", c_int32, [c_void_p, ctypes.POINTER(SvoCamera), c_int32, c_void_p, c_void_p, c_int32,
                                     c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -128,7 +130,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.svo_abi_version() != 1:
+        if L.svo_abi_version() != 2:  # include/svo_c.h SVO_ABI_VERSION
             raise SvoError(SVO_ERR_STATE, "ABI version mismatch")
         _lib = L
     return _lib

@@ -118,6 +118,12 @@ class PyramidSet:
         count = self.n_frames - first if count is None else count
         check(lib().svo_pyramid_set_build(self.handle, int(first), int(count)))
 
+    def build_async(self, first=0, count=None):
+        """build() on the context's prep stream, overlapping work queued after it (svo_pyramid_set_build_async):
+        every later use of the set through the library waits for it."""
+        count = self.n_frames - first if count is None else count
+        check(lib().svo_pyramid_set_build_async(self.handle, int(first), int(count)))
+
     def level_size(self, level):
         w, h = ctypes.c_int32(), ctypes.c_int32()
         check(lib().svo_pyramid_level_size(self.handle, int(level), ctypes.byref(w), ctypes.byref(h)))
@@ -214,7 +220,10 @@ class Point:
     def find_frame(self, frame):  # src/point.cpp: any observing feature in `frame`
         return any(f.frame is frame for f in self.features)
 
-    # always a float64 array (_feature_arrays joins the raw bytes)
+    # always a float64 array (_feature_arrays joins the raw bytes).  Setting it bumps a global version that
+    # invalidates every Frame's cached point array (a point is not told which frames' features hold it).
+    _ver = 0
+
     @property
     def position(self):
         return self._position
@@ -222,6 +231,7 @@ class Point:
     @position.setter
     def position(self, v):
         self._position = np.asarray(v, dtype=np.float64)
+        Point._ver += 1
 
 
 class Feature:
@@ -241,7 +251,14 @@ class Feature:
         self._bearing = None if bearing is None else np.asarray(bearing, np.float64)
         self.point = point
 
-    # always a float64 array (_feature_arrays joins the raw bytes)
+    def _touch(self):  # the owning frame's cached feature arrays are stale
+        fr = getattr(self, "frame", None)
+        cell = getattr(fr, "_feat_ver", None)
+        if cell is not None:
+            cell[0] += 1
+
+    # always a float64 array (_feature_arrays joins the raw bytes); assignments (not in-place edits of the array)
+    # invalidate the frame's cached arrays
     @property
     def pixel_position(self):
         return self._px
@@ -249,6 +266,16 @@ class Feature:
     @pixel_position.setter
     def pixel_position(self, v):
         self._px = np.asarray(v, dtype=np.float64)
+        self._touch()
+
+    @property
+    def point(self):
+        return self._point
+
+    @point.setter
+    def point(self, p):
+        self._point = p
+        self._touch()
 
     @property
     def bearing_vec(self):  # formed on first use (the map creates many features that never need it)
@@ -258,6 +285,36 @@ class Feature:
 
     def set_point(self, point):
         self.point = point
+
+
+class _FeatureList(list):
+    """Frame.features: a list whose mutations bump the frame's feature version (the cached SoA arrays of
+    _feature_arrays are rebuilt only after a change)."""
+    __slots__ = ("_cell",)
+
+    def __init__(self, items=(), cell=None):
+        super().__init__(items)
+        self._cell = cell
+
+    def _bump(self):
+        if self._cell is not None:
+            self._cell[0] += 1
+
+
+def _mutator(name):
+    base = getattr(list, name)
+
+    def f(self, *a, **k):
+        r = base(self, *a, **k)
+        self._bump()
+        return r if name != "__iadd__" else self
+    f.__name__ = name
+    return f
+
+
+for _m in ("append", "extend", "insert", "remove", "pop", "clear", "sort", "reverse", "__setitem__", "__delitem__",
+           "__iadd__", "__imul__"):
+    setattr(_FeatureList, _m, _mutator(_m))
 
 
 class Frame:
@@ -272,6 +329,8 @@ class Frame:
         self.camera = camera
         self.abs_pose = np.array([0, 0, 0, 1, 0, 0, 0], dtype=np.float64)  # identity (src/frame.cpp:13)
         self.image_pyramid = ImagePyramid(img, max_image_pyramid, ctx)
+        self._feat_ver = [0]  # bumped by any change to the features (list or Feature attributes)
+        self._soa = None      # (key, px, bearing, point, has_point) of the current features
         self.features = []
         self.last_keyframe = last_keyframe
         self.timestamp = timestamp
@@ -287,42 +346,73 @@ class Frame:
                                     pts.shape[0], ptr(pts), ptr(out)))
         return out if np.ndim(points) == 2 else out[0]
 
+    @property
+    def features(self):
+        return self._features
+
+    @features.setter
+    def features(self, v):
+        self._features = _FeatureList(v, self._feat_ver)
+        self._feat_ver[0] += 1
+
     def add_feature(self, feature):
         self.features.append(feature)
 
     def number_observation(self):
         return len(self.features)
 
+    def feature_arrays(self):
+        """This frame's features as SoA arrays (px, bearing, point, has_point), cached until the features change
+        (list mutations, Feature.pixel_position / point assignments, any Point.position assignment)."""
+        key = (self._feat_ver[0], Point._ver)
+        c = self._soa
+        if c is None or c[0] != key:
+            if c is not None and c[0][0] == key[0]:  # only point positions moved: keep px / bearing / has_point
+                self._soa = (key, c[1], c[2], _points_of(self.features), c[4])
+            else:
+                self._soa = (key, *_feature_soa(self.features))
+        return self._soa[1:]
+
 
 def _rows(vals, width):
     """float64 arrays of `width` values each -> an (n, width) array.  One join of their raw bytes is ~2x faster
     than np.array over the list (the per-frame gather of ~2000 features is most of align()'s host time).  Feature
-    and Point keep these attributes float64 arrays (their setters convert); a duck-typed feature must hold
-    float64 arrays too (checked on the first row and by the total length; non-arrays take np.array's
-    conversion)."""
+    and Point keep these attributes float64 arrays (their setters convert); a duck-typed feature's rows that are
+    not all float64 arrays of `width` values (checked per row and by the total length) take np.array's
+    conversion."""
     n = len(vals)
     try:
         buf = b"".join([v.tobytes() for v in vals])
-        if len(buf) == 8 * width * n and vals[0].dtype == np.float64:
+        if len(buf) == 8 * width * n and all(v.dtype == np.float64 for v in vals):
             return np.frombuffer(buf, dtype=np.float64).reshape(n, width)
     except AttributeError:
         pass
     return np.array(vals, dtype=np.float64).reshape(n, width)
 
 
-def _feature_arrays(frames):
-    """The frames' features as SoA arrays (px, bearing, point, has_point), in frame then feature order."""
-    feats = [f for fr in frames for f in fr.features]
+def _points_of(feats):
+    z = np.zeros(3)
+    return _rows([z if f.point is None else f.point.position for f in feats], 3) if feats else np.zeros((0, 3))
+
+
+def _feature_soa(feats):
     n = len(feats)
     if n == 0:
-        return np.zeros((1, 2)), np.zeros((1, 3)), np.zeros((1, 3)), np.zeros(1, np.uint8)
+        return np.zeros((0, 2)), np.zeros((0, 3)), np.zeros((0, 3)), np.zeros(0, np.uint8)
     px = _rows([f.pixel_position for f in feats], 2)
     br = _rows([f.bearing_vec for f in feats], 3)
-    pts = [f.point for f in feats]
-    hp = np.fromiter((p is not None for p in pts), dtype=np.uint8, count=n)
-    z = np.zeros(3)
-    pt = _rows([z if p is None else p.position for p in pts], 3)
-    return px, br, pt, hp
+    hp = np.fromiter((f.point is not None for f in feats), dtype=np.uint8, count=n)
+    return px, br, _points_of(feats), hp
+
+
+def _feature_arrays(frames):
+    """The frames' features as SoA arrays (px, bearing, point, has_point), in frame then feature order (each
+    frame's arrays cached by Frame.feature_arrays, so a frame that serves as ref or keyframe again costs no
+    per-feature gather)."""
+    parts = [fr.feature_arrays() for fr in frames]
+    if sum(len(p[0]) for p in parts) == 0:
+        return np.zeros((1, 2)), np.zeros((1, 3)), np.zeros((1, 3)), np.zeros(1, np.uint8)
+    return tuple(np.concatenate([p[i] for p in parts]) for i in range(4))
 
 
 MEDIAN_EXACT, MEDIAN_REFERENCE = 0, 1  # include/svo_c.h SVO_MEDIAN_*
@@ -839,7 +929,14 @@ class FeatureSelection:
         return self._emit(frame, px, resp, n.value)
 
 
-SCALE_AUTO, SCALE_K2R, SCALE_K2V = 0, 1, 2  # include/svo_c.h SVO_SCALE_*
+SCALE_AUTO, SCALE_K2R, SCALE_K2V, SCALE_K2 = 0, 1, 2, 3  # include/svo_c.h SVO_SCALE_*
+
+
+def robust_scale_capacity(impl):
+    """Largest residual vector (features x patch^2) the kernel `impl` takes (svo_robust_scale_capacity)."""
+    v = ctypes.c_int64()
+    check(lib().svo_robust_scale_capacity(int(impl), ctypes.byref(v)))
+    return int(v.value)
 SCALE_K2V_MAX_SLOTS = 98 * 512              # K2V holds the vector in registers (align_refv.hip)
 
 

@@ -1115,6 +1115,7 @@ __global__ void __launch_bounds__(kSelThreads, 4) align_scale_kernel(AlignArgs a
         S.c = 4.6851 * sigma;
         S.n = n;
         S.n_ref_vis = nrv;
+        S.scale_kernel = SVO_SCALE_K2;
     }
     K2_STAMP(15, __builtin_amdgcn_s_memrealtime());
 }
@@ -1184,6 +1185,7 @@ __device__ void pair_step(const AlignArgs& a, PairState& S, int level, int pair,
     const double e = sqrt(chi / (double)S.n);  // RMSE before the update (:366)
     t.level = level; t.n_ref_vis = (int32_t)S.n_ref_vis; t.n_vis = (int32_t)S.n; t.status = st;
     t.median = S.med; t.mad = S.mad; t.sigma = S.sigma; t.chi2 = chi; t.lambda = lambda; t.err = e;
+    t.scale_kernel = S.scale_kernel;
     for (int r = 0; r < 6; ++r) { t.g[r] = g[r]; t.dx[r] = dx[r]; }
     S.err = e;
     S.status = st;

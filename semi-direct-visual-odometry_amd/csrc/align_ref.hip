@@ -750,6 +750,7 @@ __device__ __forceinline__ void scale_ref_pair(const AlignArgs& a, int level, Re
         S.c = 4.6851 * sigma;
         S.n = n;
         S.n_ref_vis = nrv;
+        S.scale_kernel = SVO_SCALE_K2R;
     }
 }
 
@@ -808,13 +809,13 @@ int scale_impl() {
     return v;
 }
 void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s) {
-    if (scale_impl() != SVO_SCALE_K2R && (int64_t)a.max_f * a.area <= refv_max_slots()) {
+    if (scale_impl() != SVO_SCALE_K2R && (int64_t)a.max_slots <= refv_max_slots()) {
         launch_scale_refv(a, level, s);
         return;
     }
     // a launch of at most 128 pairs (small batches, one pair per frame) gives each pair a whole CU
     const bool wide = a.n_pairs <= 128;
-    const bool small = (int64_t)a.max_f * a.area <= (int64_t)kSmallM;
+    const bool small = (int64_t)a.max_slots <= (int64_t)kSmallM;
     if (small && wide) hipLaunchKernelGGL((align_scale_ref_kernel<2, 16>), dim3(a.n_pairs), dim3(Geo<16>::RT), 0, s, a, level);
     else if (small) hipLaunchKernelGGL((align_scale_ref_kernel<2, 8>), dim3(a.n_pairs), dim3(Geo<8>::RT), 0, s, a, level);
     else if (wide) hipLaunchKernelGGL((align_scale_ref_kernel<17, 16>), dim3(a.n_pairs), dim3(Geo<16>::RT), 0, s, a, level);

@@ -1389,6 +1389,7 @@ __device__ __forceinline__ void scale_refv_pair(const AlignArgs& a, VShared<R>& 
         S.c = 4.6851 * sigma;
         S.n = n;
         S.n_ref_vis = nrv;
+        S.scale_kernel = SVO_SCALE_K2V;
     }
 }
 

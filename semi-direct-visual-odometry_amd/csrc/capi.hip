@@ -67,6 +67,10 @@ struct svo_ctx {
     // on `stream`; staged: the upload is done; stage_free: the last scatter out of a staging block is done
     hipStream_t copy;
     hipEvent_t staged, stage_free;
+    // svo_pyramid_set_build_async builds on its own stream, after everything queued on `stream` so far (prep_gate),
+    // so that the next batch's pyramids build while the current batch aligns
+    hipStream_t prep = nullptr;
+    hipEvent_t prep_gate = nullptr;
     // grow-only scratch of the synchronous per-call entry points (FeatureAlignment): no device
     // allocation per call once warm
     void* scratch = nullptr;
@@ -177,7 +181,17 @@ struct svo_pyramid_set {
     svo::LevelGeom geom;
     int64_t grad_off, stride;
     uint8_t* d_base;
+    hipEvent_t ready = nullptr;  // svo_pyramid_set_build_async: recorded on the prep stream after the build
+    bool pending = false;        // a build_async whose `ready` the context stream has not waited for yet
 };
+
+// the context stream waits for the set's last asynchronous build (every user of a set's planes on the context
+// stream goes through this first: uploads, builds, downloads, and the batches' set_pair / set_pairs)
+static hipError_t set_join(svo_pyramid_set* p) {
+    if (!p || !p->pending) return hipSuccess;
+    p->pending = false;
+    return hipStreamWaitEvent(p->ctx->stream, p->ready, 0);
+}
 
 struct svo_align_batch {
     svo_ctx* ctx;
@@ -238,6 +252,8 @@ int svo_ctx_create(int32_t device, svo_ctx** out) {
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->sides[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->prep, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->prep_gate, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->stage_free, hipEventDisableTiming);
@@ -261,6 +277,9 @@ int svo_ctx_destroy(svo_ctx* c) {
     for (hipEvent_t ev : c->events)
         if (ev) (void)hipEventDestroy(ev);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
+    if (c->prep) (void)hipStreamSynchronize(c->prep);
+    if (c->prep) (void)hipStreamDestroy(c->prep);
+    if (c->prep_gate) (void)hipEventDestroy(c->prep_gate);
     if (c->fork) (void)hipEventDestroy(c->fork);
     if (c->staged) (void)hipEventDestroy(c->staged);
     if (c->stage_free) (void)hipEventDestroy(c->stage_free);
@@ -333,6 +352,10 @@ int svo_pyramid_set_destroy(svo_pyramid_set* p) {
     if (!p) return SVO_OK;
     (void)hipSetDevice(p->ctx->device);
     (void)hipStreamSynchronize(p->ctx->stream);
+    if (p->ready) {
+        (void)hipStreamSynchronize(p->ctx->prep);
+        (void)hipEventDestroy(p->ready);
+    }
     (void)hipFree(p->d_base);
     delete p;
     return SVO_OK;
@@ -342,6 +365,7 @@ static int upload_impl(svo_pyramid_set* p, int32_t first, int32_t count, const u
     if (!p || !src) return fail(SVO_ERR_ARG, "null argument");
     if (first < 0 || count < 0 || first + count > p->n_frames) return fail(SVO_ERR_ARG, "frames out of range");
     SVO_HIP(hipSetDevice(p->ctx->device));
+    SVO_HIP(set_join(p));
     const size_t img = (size_t)p->width * p->height;
     SVO_HIP(hipMemcpy2DAsync(p->d_base + (size_t)first * p->stride, (size_t)p->stride, src, img, img, count, kind,
                              p->ctx->stream));
@@ -361,8 +385,27 @@ int svo_pyramid_set_build(svo_pyramid_set* p, int32_t first, int32_t count) {
     if (first < 0 || count < 0 || first + count > p->n_frames) return fail(SVO_ERR_ARG, "frames out of range");
     if (count == 0) return SVO_OK;
     SVO_HIP(hipSetDevice(p->ctx->device));
+    SVO_HIP(set_join(p));
     svo::launch_pyramid(p->d_base, p->geom, first, count, p->ctx->stream);
     SVO_HIP(hipGetLastError());
+    return SVO_OK;
+}
+
+int svo_pyramid_set_build_async(svo_pyramid_set* p, int32_t first, int32_t count) {
+    if (!p) return fail(SVO_ERR_ARG, "null argument");
+    if (first < 0 || count < 0 || first + count > p->n_frames) return fail(SVO_ERR_ARG, "frames out of range");
+    if (count == 0) return SVO_OK;
+    svo_ctx* c = p->ctx;
+    SVO_HIP(hipSetDevice(c->device));
+    if (!p->ready) SVO_HIP(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+    // after everything the context stream holds now (the uploads of these frames, and the alignment that
+    // last read the planes), and after an earlier asynchronous build of this set (the prep stream is in order)
+    SVO_HIP(hipEventRecord(c->prep_gate, c->stream));
+    SVO_HIP(hipStreamWaitEvent(c->prep, c->prep_gate, 0));
+    svo::launch_pyramid(p->d_base, p->geom, first, count, c->prep);
+    SVO_HIP(hipGetLastError());
+    SVO_HIP(hipEventRecord(p->ready, c->prep));
+    p->pending = true;
     return SVO_OK;
 }
 
@@ -370,6 +413,7 @@ int svo_pyramid_set_download(const svo_pyramid_set* p, int32_t frame, int32_t le
     if (!p || !out) return fail(SVO_ERR_ARG, "null argument");
     if (frame < 0 || frame >= p->n_frames || level < 0 || level >= p->levels) return fail(SVO_ERR_ARG, "index out of range");
     SVO_HIP(hipSetDevice(p->ctx->device));
+    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(p)));
     const uint8_t* src = p->d_base + (size_t)frame * p->stride + (gradient ? p->grad_off : 0) + p->geom.off[level];
     SVO_HIP(hipMemcpyAsync(out, src, (size_t)p->geom.w[level] * p->geom.h[level], hipMemcpyDeviceToHost, p->ctx->stream));
     SVO_HIP(hipStreamSynchronize(p->ctx->stream));
@@ -508,6 +552,9 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
     if ((rc = check_frame(b, kf_set, kf_frame)) != SVO_OK) return rc;
     if ((rc = check_frame(b, cur_set, cur_frame)) != SVO_OK) return rc;
     SVO_HIP(hipSetDevice(b->ctx->device));
+    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(ref_set)));
+    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(kf_set)));
+    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(cur_set)));
     svo::PairDesc& d = b->h_pairs[pair];
     d.ref_pyr = ref_set->d_base + (size_t)ref_frame * ref_set->stride;
     d.kf_pyr = kf_set->d_base + (size_t)kf_frame * kf_set->stride;
@@ -605,6 +652,9 @@ int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, 
     const int64_t T = off[count];
     if (T > 0 && (!px || !bearing || !point || !has_point)) return fail(SVO_ERR_ARG, "null feature array");
     SVO_HIP(hipSetDevice(b->ctx->device));
+    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(ref_set)));
+    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(kf_set)));
+    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(cur_set)));
     for (int32_t i = 0; i < count; ++i) {
         svo::PairDesc& d = b->h_pairs[first + i];
         d.ref_pyr = ref_set->d_base + (size_t)frames[3 * i] * ref_set->stride;
@@ -686,6 +736,15 @@ int svo_align_batch_set_initial_poses(svo_align_batch* b, const double* poses) {
     return SVO_OK;
 }
 
+// the largest residual vector (n_ref + n_kf) * patch area among pairs [p0, p0 + n): the reference-mode robust
+// scale kernel is chosen per launch by the vectors the pairs actually hold (src/image_alignment.cpp:30-38 sizes
+// the vector per frame), not by the batch's capacity
+static int32_t batch_max_slots(const svo_align_batch* b, int32_t p0, int32_t n) {
+    int32_t m = 0;
+    for (int32_t i = p0; i < p0 + n; ++i) m = std::max(m, b->h_pairs[i].n_ref + b->h_pairs[i].n_kf);
+    return m * b->area;
+}
+
 // Pairs [p0, p0 + n) of a batch as a batch of their own (every per-pair array offset by p0).
 static svo::AlignArgs sub_batch(const svo::AlignArgs& a, const svo_align_batch* b, int32_t p0, int32_t n) {
     svo::AlignArgs s = a;
@@ -702,6 +761,7 @@ static svo::AlignArgs sub_batch(const svo::AlignArgs& a, const svo_align_batch* 
     s.traces += (int64_t)p0 * (b->params.max_level + 1);
     s.n_pairs = n;
     s.pair_base = a.pair_base + p0;
+    s.max_slots = batch_max_slots(b, p0, n);
     return s;
 }
 
@@ -720,6 +780,7 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     a.feat_iters = b->feat_iters; a.chunks = b->chunks; a.fvis = b->d_fvis; a.cproj = b->d_cproj; a.scratch = b->d_scratch;
     a.pose_out = b->d_pose_out; a.err_out = b->d_err; a.status_out = b->d_status; a.traces = b->d_traces;
     a.n_pairs = b->n_pairs; a.pair_base = 0; a.max_f = b->max_f; a.half = b->half; a.area = b->area;
+    a.max_slots = batch_max_slots(b, 0, b->n_pairs);
     a.min_level = b->params.min_level; a.max_level = b->params.max_level;
     a.fx = b->cam.fx; a.fy = b->cam.fy; a.cx = b->cam.cx; a.cy = b->cam.cy;
     a.geom = b->geom;
@@ -743,7 +804,7 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         // K2V (the default reference-mode kernel whenever the vector fits its registers) fills whole CUs, so
         // the other chain's K1 / K3 run only between its launches whatever the stagger: unstaggered measured
         // best (MI355X, 512 pairs: stagger 0 / 1 / 2 / 3 = 119.1k / 118.4k / 117.3k / 117.4k pairs/s).
-        const bool k2v = svo::scale_impl() != SVO_SCALE_K2R && (int64_t)b->max_f * b->area <= svo::refv_max_slots();
+        const bool k2v = svo::scale_impl() != SVO_SCALE_K2R && (int64_t)a.max_slots <= svo::refv_max_slots();
         const int stagger = env_stagger >= 0 ? env_stagger
                                              : (b->params.median_mode == SVO_MEDIAN_REFERENCE && !k2v ? 2 : 0);
         if (stagger < 0 || stagger > 1 + 3 * (b->params.max_level - b->params.min_level + 1))
@@ -838,6 +899,14 @@ int svo_align_batch_traces(svo_align_batch* b, int32_t pair, svo_level_trace* ou
     (void)hipGetLastError();
     SVO_HIP(hipMemcpyAsync(out, b->d_traces + (size_t)pair * L, bytes, hipMemcpyDeviceToHost, c->stream));
     SVO_HIP(hipStreamSynchronize(c->stream));
+    return SVO_OK;
+}
+
+int svo_robust_scale_capacity(int32_t impl, int64_t* slots) {
+    if (!slots) return fail(SVO_ERR_ARG, "null argument");
+    if (impl == SVO_SCALE_K2V) *slots = svo::refv_max_slots();
+    else if (impl == SVO_SCALE_K2R) *slots = SVO_REF_MAX_SLOTS;
+    else return fail(SVO_ERR_ARG, "impl %d has no capacity (SVO_SCALE_K2V or SVO_SCALE_K2R)", impl);
     return SVO_OK;
 }
 

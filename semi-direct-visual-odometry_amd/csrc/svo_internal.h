@@ -32,6 +32,7 @@ struct PairState {  // per frame pair, carried from stage to stage and level to 
     double err;                 // RMSE of the last finished level
     uint32_t n, n_ref_vis;      // visible pixel slots / ref-visible features of the current level
     int32_t status, active;     // Optimizer::Status of the last level; 0 = nothing to align
+    int32_t scale_kernel, pad;  // SVO_SCALE_* of the kernel that computed med / mad at the current level
 };
 
 struct AlignArgs {
@@ -66,6 +67,8 @@ struct AlignArgs {
     int32_t* status_out;      // [n_pairs]
     svo_level_trace* traces;  // [n_pairs][max_level+1]
     int32_t n_pairs, max_f, half, area, min_level, max_level;
+    int32_t max_slots;        // largest (n_ref + n_kf) * area over these pairs: the reference-mode robust scale
+                              // kernel is chosen by it (K2V when it fits), not by the batch capacity max_f
     int32_t pair_base;        // index of pair 0 of these arguments in the whole batch (sub-batch chains)
     int32_t feat_iters;       // feature groups one K1/K3 wave walks through
     int32_t chunks;           // K1/K3 workgroups per pair = align_chunks(max_f, half, feat_iters)

@@ -38,7 +38,7 @@ def test_ctypes_table_matches_header():
 
 def test_errors_are_codes():
     L = _capi.lib()
-    assert L.svo_abi_version() == 1
+    assert L.svo_abi_version() == 2
     h = ctypes.c_void_p()
     assert L.svo_pyramid_set_create(None, 1, 64, 64, 3, ctypes.byref(h)) == _capi.SVO_ERR_ARG
     assert b"null" in L.svo_last_error()
