@@ -59,7 +59,8 @@ def parse():
                          "row, src/feature_selection.cpp:103-141); shuffled: random order")
     ap.add_argument("--median", choices=("reference", "exact"), default="reference",
                     help="robust-scale semantics: reference = the reference's libstdc++ nth_element post-state "
-                         "(median_mode SVO_MEDIAN_REFERENCE, K2R); exact = true order statistics (K2)")
+                         "(median_mode SVO_MEDIAN_REFERENCE: K2V, the vector in registers; K2R past its capacity); "
+                         "exact = true order statistics (K2)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the config 3 / config 5 lines")
     ap.add_argument("--core-only", action="store_true",

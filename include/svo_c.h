@@ -64,7 +64,9 @@ typedef struct {
  * algorithm::computeMedian / computeMAD, src/algorithm.cpp:834-865).
  *   SVO_MEDIAN_REFERENCE: the reference's own values: std::nth_element on the full residual vector and,
  *     for an even length, vec[n/2 - 1] as libstdc++'s introselect leaves it (not always the (n/2 - 1)-th
- *     order statistic): the device re-runs the introselect (K2R, csrc/align_ref.hip);
+ *     order statistic): the device re-runs the introselect -- K2V (csrc/align_refv.hip, the vector in one
+ *     CU's registers) whenever every pair of a launch holds at most svo_robust_scale_capacity(SVO_SCALE_K2V)
+ *     slots, K2R (csrc/align_ref.hip, segments in LDS / global scratch) otherwise; the same bits either way;
  *   SVO_MEDIAN_EXACT: true order statistics ((n/2 - 1)-th and n/2-th), the robust statistic the
  *     reference means; faster (K2). */
 enum { SVO_MEDIAN_EXACT = 0, SVO_MEDIAN_REFERENCE = 1 };

@@ -56,7 +56,8 @@ struct AlignArgs {
     uint16_t* keys;           // scratch [n_pairs][key_stride] 16-bit monotone key per slot (0xFFFF = invisible)
     uint32_t* sel;            // median_mode 1: [n_pairs][sel_stride] K2R scratch (segment, mailbox, step records)
     int64_t sel_stride;       // u32 per pair: ref_sel_stride(max_f * area)
-    int32_t median_mode;      // 0 exact order statistics (K2), 1 the reference's nth_element post-state (K2R)
+    int32_t median_mode;      // 0 exact order statistics (K2), 1 the reference's nth_element post-state (K2V, or
+                              // K2R for vectors past K2V's registers: launch_scale_ref chooses by max_slots)
     int64_t key_stride;       // >= area * round_up(max_f, 64), multiple of 64
     uint32_t* win;            // scratch [n_pairs][win_stride] feature windows of the window levels (K1 -> K3)
     int64_t win_stride;       // dwords per pair: align_win_dwords(half) * round_up(max_f, 64)

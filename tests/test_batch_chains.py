@@ -108,9 +108,9 @@ def test_gpu_two_chain_batch(mode):
 
 @pytest.mark.gpu
 def test_gpu_wide_launch_instantiation():
-    """Launches of more than 128 pairs run K2R's 8-wave instantiation (two pairs per CU, the headline's);
-    smaller ones the 16-wave one.  264 pairs = two chains of 136: every pair against the oracle's
-    std::nth_element path and bit for bit against a single-pair (16-wave) run of its scene."""
+    """Two chains of 132 pairs (the 2000-feature vectors fit K2V, so both chains run it; trace field
+    scale_kernel): every pair against the oracle's std::nth_element path and bit for bit against a single-pair
+    run of its scene.  K2R's own batch instantiations are covered by tests/test_config4.py."""
     ctx = svo_amd.default_context()
     sc = scenes()
     ps = pyramids(sc, ctx)

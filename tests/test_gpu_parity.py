@@ -258,3 +258,41 @@ def test_feature_align_large_batch_pageable_staging():
     px_g = np.ascontiguousarray(init.copy())
     err_g, st_g = svo_amd.FeatureAlignment(7).align_batch(ps, 0, ps, 1, ref_px, px_g, svo_amd.PinholeCamera.kitti())
     assert np.array_equal(px_g, px_c) and np.array_equal(st_g, st_c)
+
+
+def test_pyramid_build_async_pipeline():
+    """svo_pyramid_set_build_async (the prep stream): a set built asynchronously while a batch aligns on another
+    set gives the oracle's bytes, and a batch handed the async-built set (set_pairs waits for the build) aligns
+    exactly as one built synchronously (bench.py end_to_end_device_images pipelines batches this way)."""
+    sc = make_pairs(2)
+    cam = svo_amd.PinholeCamera.kitti()
+    imgs = np.stack([im for s in sc for im in (s.ref_img, s.kf_img, s.cur_img)])
+    A = svo_amd.PyramidSet(6, 1241, 376, 5)
+    B = svo_amd.PyramidSet(6, 1241, 376, 5)
+    A.upload(0, imgs)
+    B.upload(0, imgs)
+    A.build()
+    b = svo_amd.AlignBatch(cam, 5, 0, 4, 2, 2000, median_mode=svo_amd.MEDIAN_REFERENCE)
+    frames = np.arange(6, dtype=np.int32).reshape(2, 3)
+    poses = np.stack([np.concatenate([s.ref_pose, s.kf_pose, s.cur_init_pose]) for s in sc])
+    n_feat = np.array([[s.n_ref, s.n_kf] for s in sc], np.int32)
+    cat = lambda f: np.concatenate([getattr(s, f) for s in sc])
+    feats = (cat("px"), cat("bearing"), cat("point"), cat("has_point"))
+    b.set_pairs(0, A, A, A, frames, poses, n_feat, *feats)
+    B.build_async()  # overlaps the alignment queued next
+    b.run()
+    pa, ea, sa = b.results()
+    for i, im in enumerate(imgs[:3]):
+        oi, og = O.build_pyramid(im, 5)
+        li, lg = O.unpack_levels(oi, 1241, 376, 5), O.unpack_levels(og, 1241, 376, 5)
+        for l in range(5):
+            assert np.array_equal(B.download(i, l, False), li[l]) and np.array_equal(B.download(i, l, True), lg[l])
+    A.build_async()  # rebuild A while B serves the next batch
+    b.set_pairs(0, B, B, B, frames, poses, n_feat, *feats)
+    b.run()
+    pb, eb, sb = b.results()
+    assert np.array_equal(pa, pb) and np.array_equal(ea, eb) and np.array_equal(sa, sb)
+    b.set_pairs(0, A, A, A, frames, poses, n_feat, *feats)  # waits for A's async build
+    b.run()
+    pc, _, _ = b.results()
+    assert np.array_equal(pa, pc)

@@ -21,7 +21,9 @@ for step in "$@"; do
         quick) run quick 300 python3 tests/gpu_smoke.py ;;
         tests) run tests 900 python3 -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         bench) run bench 600 python3 bench.py ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu
+              # the longest dispatches of the same trace, committed beside every kernel-stats summary
+              python3 tools/top_dispatches.py gpurun_out/prof/run_kernel_trace.csv 10 > gpurun_out/top_dispatches.txt && cat gpurun_out/top_dispatches.txt ;;
         pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-secondary --core-only
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-secondary --core-only
              python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/pmc_traffic.json && cat gpurun_out/pmc_traffic.json ;;
