@@ -190,8 +190,9 @@ int svo_align_batch_results(svo_align_batch* batch, double* poses, double* err, 
 int svo_align_batch_traces(svo_align_batch* batch, int32_t pair, svo_level_trace* out);
 
 /* Device forms of the reference robust scale (SVO_MEDIAN_REFERENCE): K2V keeps the residual vector in
- * registers (vectors of <= 50 176 slots: config 2's 2000 features x 25), K2R runs its large rounds through
- * global scratch (any size).  Both give the same bits. */
+ * registers (vectors of <= 60 416 slots, 2416 features at patch 5; the faster of its two register layouts up
+ * to 50 176 slots, config 2's 2000 features x 25), K2R runs its large rounds through global scratch (any size).
+ * Both give the same bits. */
 enum { SVO_SCALE_AUTO = 0, SVO_SCALE_K2R = 1, SVO_SCALE_K2V = 2, SVO_SCALE_K2 = 3 /* exact mode (trace only) */ };
 
 /* Diagnostics (no reference counterpart): the SVO_MEDIAN_REFERENCE robust scale of an arbitrary residual
@@ -203,6 +204,8 @@ enum { SVO_SCALE_AUTO = 0, SVO_SCALE_K2R = 1, SVO_SCALE_K2V = 2, SVO_SCALE_K2 = 
  *   K2R: with the environment variable SVO_DEBUG_STAMPS set, [2..9] cycles / block rounds / one-wave rounds
  *        / heap select per pass, [10..189] the block rounds, [190..205] cycles per round phase
  *        (tools/k2r_probe.py).
+ * K2V with out_len > 206: out[206..] receives a round trace (development): per round 8 header doubles (pass + 10
+ * kind, f, l, pivot, Ks, #GE, #LE, cut) and the vector's n_slots values after the round.
  * Synchronous.  SVO_ERR_ARG if impl is K2V and the vector does not fit it. */
 int svo_debug_robust_scale(svo_ctx* ctx, const double* values, int64_t n_slots, int64_t n_valid, int32_t impl,
                            double* out, int64_t out_len);

@@ -927,7 +927,9 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
     const int64_t sel_stride = svo::ref_sel_stride(n_slots);  // u32
     const int64_t q = (n_slots + 63) / 64 * 64;
     constexpr int64_t kDiag = 206;  // the diagnostics either kernel writes
-    const size_t bytes = (size_t)q * 8 + (size_t)sel_stride * 4 + kDiag * 8;
+    // out_len past kDiag: K2V's round trace (development; align_refv.hip VDiag::tr) in the rest of out
+    const int64_t ntr = impl == SVO_SCALE_K2V && out_len > kDiag ? std::min<int64_t>(out_len - kDiag, 1ll << 28) : 0;
+    const size_t bytes = (size_t)q * 8 + (size_t)sel_stride * 4 + (size_t)(kDiag + ntr) * 8;
     void* base = nullptr;
     hipError_t e = ctx_scratch(c, bytes, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_debug_robust_scale: %s", hipGetErrorString(e));
@@ -935,13 +937,13 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
     double* d_v = static_cast<double*>(base);
     uint32_t* d_sel = reinterpret_cast<uint32_t*>(d_v + q);
     double* d_out = reinterpret_cast<double*>(d_sel + sel_stride);
-    SVO_HIP(hipMemsetAsync(d_out, 0, kDiag * 8, c->stream));
+    SVO_HIP(hipMemsetAsync(d_out, 0, (size_t)(kDiag + ntr) * 8, c->stream));
     SVO_HIP(hipMemcpyAsync(d_v, values, (size_t)n_slots * 8, hipMemcpyHostToDevice, c->stream));
     if (svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, sel_stride, impl, d_out,
-                                       c->stream) != 0)
+                                       ntr ? d_out + kDiag : nullptr, (uint32_t)ntr, c->stream) != 0)
         return fail(SVO_ERR_ARG, "the vector does not fit the requested kernel");
     SVO_HIP(hipGetLastError());
-    SVO_HIP(hipMemcpyAsync(out, d_out, (size_t)std::min<int64_t>(out_len, kDiag) * 8, hipMemcpyDeviceToHost, c->stream));
+    SVO_HIP(hipMemcpyAsync(out, d_out, (size_t)std::min<int64_t>(out_len, kDiag + ntr) * 8, hipMemcpyDeviceToHost, c->stream));
     SVO_HIP(hipStreamSynchronize(c->stream));
     return SVO_OK;
 }

@@ -1,5 +1,5 @@
 """The reference's robust scale bit for bit: median_mode SVO_MEDIAN_REFERENCE (K2V, csrc/align_refv.hip, for
-vectors of <= 50 176 slots; K2R, csrc/align_ref.hip, for any size).
+vectors of <= 60 416 slots in two register layouts; K2R, csrc/align_ref.hip, for any size).
 
 algorithm::computeMedian (src/algorithm.cpp:834-853) runs std::nth_element on the full residual vector and
 reads vec[n/2 - 1] from libstdc++'s post-partition state.  K2R re-runs that introselect on the device.
@@ -97,15 +97,17 @@ def test_debug_robust_scale_matches_nth_element(case, impl):
 
 @pytest.mark.gpu
 def test_debug_robust_scale_k2v_extremes():
-    """K2V at its capacity (50 176 slots: every register row and LDS row in use), a vector whose first
-    round needs a chunked exchange (Ks > the 12 288-slot mailbox: reversed order), all-invisible tails, and
-    n_valid far below the length."""
+    """K2V at the capacity of each register layout (LayA 50 176 slots, LayB 60 416: every register row and LDS
+    row in use), vectors whose first round needs a chunked exchange (Ks > the mailbox: reversed order; LayB's
+    4 352-slot mailbox chunks most of its first rounds), all-invisible tails, and n_valid far below the length."""
     rng = np.random.default_rng(11)
     cases = []
-    v = rng.normal(0, 8, svo_amd.SCALE_K2V_MAX_SLOTS)
-    v[np.repeat(rng.random(svo_amd.SCALE_K2V_MAX_SLOTS // 25 + 1) < 0.2, 25)[:len(v)]] = DBL_MAX
-    cases.append(v)
+    for cap in (svo_amd.SCALE_K2V_LAYA_SLOTS, svo_amd.SCALE_K2V_MAX_SLOTS):
+        v = rng.normal(0, 8, cap)
+        v[np.repeat(rng.random(cap // 25 + 1) < 0.2, 25)[:len(v)]] = DBL_MAX
+        cases.append(v)
     cases.append(np.arange(50000, 0, -1, dtype=np.float64) * 0.01)  # descending: maximal swaps per round
+    cases.append(np.arange(60000, 0, -1, dtype=np.float64) * 0.01)  # (LayB)
     cases.append(np.concatenate([rng.normal(0, 3, 30000), np.full(20000, DBL_MAX)]))
     w = rng.normal(0, 3, 40000)
     w[rng.random(40000) < 0.9] = DBL_MAX
@@ -117,7 +119,7 @@ def test_debug_robust_scale_k2v_extremes():
         med_c, mad_c = oracle_med_mad(v, n)
         assert med == med_c and mad == mad_c, (len(v), n, med, med_c, mad, mad_c, dg[:10])
         chunked.append(dg[4] + dg[9])  # block rounds whose exchange ran in mailbox chunks (both passes)
-    assert chunked[1] >= 1, chunked  # the descending vector exercises the chunked exchange
+    assert chunked[2] >= 1 and chunked[3] >= 1, chunked  # the descending vectors exercise the chunked exchange
 
 
 @pytest.mark.gpu

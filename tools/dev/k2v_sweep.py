@@ -24,7 +24,7 @@ bad = 0
 tot = 0
 for seed in range(int(sys.argv[1]) if len(sys.argv) > 1 else 40):
     rng = np.random.default_rng(1000 + seed)
-    for nf in (40, 400, 1200, 1700, 1800, 2000):
+    for nf in (40, 400, 1200, 1700, 1800, 2000, 2007, 2100, 2416):
         for pv in (1.0, 0.8):
             v = rng.normal(0, 8, nf * 25)
             vis = np.repeat(rng.random(nf) < pv, 25)
@@ -41,3 +41,4 @@ for seed in range(int(sys.argv[1]) if len(sys.argv) > 1 else 40):
                 print(f"seed {seed} nf {nf} pv {pv}: K2V med {m!r} mad {d!r} | oracle {mc!r} {dc!r} | K2R ok {m2 == mc and d2 == dc} "
                       f"| med ok {m == mc} | diag {dg[:10].tolist()}", flush=True)
 print(f"{bad} / {tot} mismatches")
+sys.exit(3 if bad else 0)
