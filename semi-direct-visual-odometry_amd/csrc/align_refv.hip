@@ -158,6 +158,12 @@ struct VSel {
     static constexpr int kGenQuads = G::kGenQuads;
     static constexpr uint32_t kMbCap = L::kMbCap;
     static constexpr int kQuads = (R + 3) / 4;  // quads of rows the block rounds walk (kGenQuads of them in registers)
+    // below this many rows a wave classifies and exchanges row by row (indexed registers) instead of walking the quads
+    static constexpr int kFewRows = 8;
+#ifndef SVO_QG
+#define SVO_QG 4
+#endif
+    static constexpr int kQG = SVO_QG;  // quads per range-tested group in the classify / exchange walks
     static constexpr bool kStampOn = L::kPreload;  // (stamps build: LayA only; LayB's registers leave no room)
     static __device__ __forceinline__ double vget(int r) { return G::vget(r); }
     static __device__ __forceinline__ void vset(int r, double x) { G::vset(r, x); }
@@ -297,6 +303,10 @@ struct VSel {
     __device__ __forceinline__ void cls_quad(double p, int rlo, int rhi, uint32_t (&acc)[2][4]) {
         opaque(rlo, rhi);  // (the quad's test here, not hoisted for all quads and spilled)
         if (4 * Q + 3 < rlo || 4 * Q > rhi) return;
+        cls_quad_in<Q>(p, acc);
+    }
+    template <int Q>
+    __device__ __forceinline__ void cls_quad_in(double p, uint32_t (&acc)[2][4]) {
         constexpr int g = (4 * Q) >> 6;  // (a quad never straddles two row groups)
         if constexpr (Q < kGenQuads) {
             G::template cls4<Q>(p, acc[g]);
@@ -314,10 +324,44 @@ struct VSel {
             }
         }
     }
-    template <int... Qs>
+    // quads in groups of four (16 rows): a group outside [rlo, rhi] costs one test instead of four
+    template <int Gq, int... Is>
+    __device__ __forceinline__ void cls_group(double p, int rlo, int rhi, uint32_t (&acc)[2][4],
+                                              std::integer_sequence<int, Is...>) {
+        opaque(rlo, rhi);
+        constexpr int r0 = 4 * kQG * Gq, r1 = r0 + 4 * (int)sizeof...(Is) - 1;
+        if (r1 < rlo || r0 > rhi) return;
+        if (r0 >= rlo && r1 <= rhi) (cls_quad_in<kQG * Gq + Is>(p, acc), ...);  // the whole group: no quad tests
+        else (cls_quad<kQG * Gq + Is>(p, rlo, rhi, acc), ...);
+    }
+    template <int... Gs>
     __device__ __forceinline__ void cls_quads(double p, int rlo, int rhi, uint32_t (&acc)[2][4],
-                                              std::integer_sequence<int, Qs...>) {
-        (cls_quad<Qs>(p, rlo, rhi, acc), ...);
+                                              std::integer_sequence<int, Gs...>) {
+        (cls_group<Gs>(p, rlo, rhi, acc, std::make_integer_sequence<int, (kQuads - kQG * Gs < kQG ? kQuads - kQG * Gs : kQG)>{}), ...);
+    }
+    // a few rows: one indexed compare pair per row instead of a pass over every quad's range test
+    __device__ __forceinline__ void cls_rows(double p, int rlo, int rhi, uint32_t (&acc)[2][4]) {
+        for (int r = rlo; r <= rhi; ++r) {
+            uint64_t ge, le;
+            if (r < kVRegRows) {
+                G::vcmp2(r, p, ge, le);
+            } else {
+                const double x = sh.lrow[r - kVRegRows][tid];
+                ge = __ballot(!(x < p));
+                le = __ballot(!(p < x));
+            }
+            // (a select per lane, not v_writelane: a runtime lane index would go through M0, which the indexed
+            // row accesses overwrite)
+            const bool mine = lane == (r & 63);
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                if (g != (r >> 6)) continue;
+                acc[g][0] = mine ? (uint32_t)ge : acc[g][0];
+                acc[g][1] = mine ? (uint32_t)(ge >> 32) : acc[g][1];
+                acc[g][2] = mine ? (uint32_t)le : acc[g][2];
+                acc[g][3] = mine ? (uint32_t)(le >> 32) : acc[g][3];
+            }
+        }
     }
     __device__ __forceinline__ void classify(double p, uint32_t ch, double x0) {
         // std::iter_swap(first, chosen) of __move_median_to_first, in the owners' registers
@@ -326,7 +370,8 @@ struct VSel {
         const WaveRows w = wave_segment(f >> 6, (l - 1) >> 6);
         uint32_t acc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};  // lane j: row 64 g + j: GE lo, GE hi, LE lo, LE hi
         if (w.rlo <= w.rhi) {
-            cls_quads(p, w.rlo, w.rhi, acc, std::make_integer_sequence<int, kQuads>{});
+            if (w.rhi - w.rlo < kFewRows) cls_rows(p, w.rlo, w.rhi, acc);
+            else cls_quads(p, w.rlo, w.rhi, acc, std::make_integer_sequence<int, (kQuads + kQG - 1) / kQG>{});
             // rows outside [rlo, rhi] (whole quads were compared) and the partial first / last rows
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
@@ -530,14 +575,44 @@ struct VSel {
             }
         }
     }
-    template <bool kWrite, int S, int... Qs>
-    __device__ __forceinline__ void ex_quads(const Ctl& C, double p, int ra, int rb, std::integer_sequence<int, Qs...>) {
+    // a quad wholly inside the range: every row takes part, no test
+    template <int Q, bool kWrite, int S>
+    __device__ __forceinline__ void ex_quad_in(const Ctl& C, double p, const uint32_t (&pb)[2]) {
+        constexpr int g = (4 * Q) >> 6;
+        if constexpr (Q < kGenQuads) {
+            if (kWrite) G::template src4<Q, S>(p, pb[g]);
+            else G::template tgt4<Q, S>(p, pb[g]);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int r = 4 * Q + i;
+                if (r < R) generic_row<kWrite>(C, S, r, ~0ull, p, 0u, kMbCap, false);
+            }
+        }
+    }
+    template <bool kWrite, int S>
+    __device__ __forceinline__ void ex_quads(const Ctl& C, double p, int ra, int rb) {
         const uint32_t mb = (uint32_t)(uintptr_t)sh.mbx;
         uint32_t pb[2];
 #pragma unroll
         for (int g = 0; g < 2; ++g)
             pb[g] = S == 0 ? mb + 8u * (C.pw[g] & 0xFFFFu) : mb + 8u * (C.totL - 1u - (C.pw[g] >> 16));
-        (ex_quad<Qs, kWrite, S>(C, p, ra, rb, pb), ...);
+        ex_groups<kWrite, S>(C, p, ra, rb, pb, std::make_integer_sequence<int, (kQuads + kQG - 1) / kQG>{});
+    }
+    template <bool kWrite, int S, int Gq, int... Is>
+    __device__ __forceinline__ void ex_group(const Ctl& C, double p, int ra, int rb, const uint32_t (&pb)[2],
+                                             std::integer_sequence<int, Is...>) {
+        opaque(ra, rb);
+        constexpr int r0 = 4 * kQG * Gq, r1 = r0 + 4 * (int)sizeof...(Is) - 1;
+        if (r1 < ra || r0 > rb) return;
+        if (r0 >= ra && r1 <= rb) (ex_quad_in<kQG * Gq + Is, kWrite, S>(C, p, pb), ...);  // whole group inside
+        else (ex_quad<kQG * Gq + Is, kWrite, S>(C, p, ra, rb, pb), ...);
+    }
+    template <bool kWrite, int S, int... Gs>
+    __device__ __forceinline__ void ex_groups(const Ctl& C, double p, int ra, int rb, const uint32_t (&pb)[2],
+                                              std::integer_sequence<int, Gs...>) {
+        (ex_group<kWrite, S, Gs>(C, p, ra, rb, pb,
+                                 std::make_integer_sequence<int, (kQuads - kQG * Gs < kQG ? kQuads - kQG * Gs : kQG)>{}), ...);
     }
     template <bool kWrite>
     __device__ __forceinline__ void exchange(const Ctl& C, int side, uint32_t s0, uint32_t s1, uint32_t bstep, double p,
@@ -557,8 +632,12 @@ struct VSel {
         (void)bstep;
         const int ra = w.rlo + 1, rb = w.rhi - 1;
         if (ra > rb) return;
-        if (side == 0) ex_quads<kWrite, 0>(C, p, ra, rb, std::make_integer_sequence<int, kQuads>{});
-        else ex_quads<kWrite, 1>(C, p, ra, rb, std::make_integer_sequence<int, kQuads>{});
+        if (rb - ra < kFewRows) {  // a few rows: the generic way, no pass over every quad's range test
+            for (int r = ra; r <= rb; ++r) generic_row<kWrite>(C, side, r, ~0ull, p, 0u, kMbCap, false);
+            return;
+        }
+        if (side == 0) ex_quads<kWrite, 0>(C, p, ra, rb);
+        else ex_quads<kWrite, 1>(C, p, ra, rb);
     }
 
     // ------------------------------------------------------------------ one block round

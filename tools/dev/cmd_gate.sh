@@ -3,6 +3,11 @@
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+for n in 50000 60000; do
+  timeout -k 10 150 python3 tools/dev/k2v_trace.py $n > gpurun_out/g_trace$n.log 2>&1; rc=$?
+  echo "trace $n rc=$rc"; grep -v "^round" gpurun_out/g_trace$n.log
+  [ $rc -ne 0 ] && exit $rc
+done
 timeout -k 10 150 python3 tools/k2r_probe.py 2 > gpurun_out/g_probe.log 2>&1; rc=$?
 echo "probe rc=$rc"; cat gpurun_out/g_probe.log
 [ $rc -ne 0 ] && exit $rc
