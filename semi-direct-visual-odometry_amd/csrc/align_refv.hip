@@ -212,11 +212,29 @@ struct VSel {
     }
     // this thread's rows of src: registers and LDS rows
     __device__ __forceinline__ void load_raw(const double* src) {
-        G::load(src, M * 8u, tid);  // (rows past M hold 0: never inside a segment)
+        constexpr int kL = R - kVRegRows;
+        if constexpr (kL <= 12) {
+            // the LDS rows' loads go out first and land during the register rows' loads (whose asm block ends
+            // with vmcnt(0)); one latency instead of one per pair of rows
+            double x[kL];
+#pragma unroll
+            for (int i = 0; i < kL; ++i) {
+                const uint32_t q = (uint32_t)(kVRegRows + i) * kVT + (uint32_t)tid;
+                x[i] = __builtin_nontemporal_load(src + (q < M ? q : 0u));
+            }
+            G::load(src, M * 8u, tid);  // (rows past M hold 0: never inside a segment)
+#pragma unroll
+            for (int i = 0; i < kL; ++i) {
+                const uint32_t q = (uint32_t)(kVRegRows + i) * kVT + (uint32_t)tid;
+                sh.lrow[i][tid] = q < M ? x[i] : 0.0;
+            }
+        } else {
+            G::load(src, M * 8u, tid);
 #pragma unroll 2
-        for (int r = kVRegRows; r < R; ++r) {
-            const uint32_t q = (uint32_t)r * kVT + (uint32_t)tid;
-            sh.lrow[r - kVRegRows][tid] = q < M ? src[q] : 0.0;
+            for (int r = kVRegRows; r < R; ++r) {
+                const uint32_t q = (uint32_t)r * kVT + (uint32_t)tid;
+                sh.lrow[r - kVRegRows][tid] = q < M ? src[q] : 0.0;
+            }
         }
     }
     // waves 1..7, during wave 0's one-wave rounds: wave 0's rows of src into LDS, the register rows to
@@ -800,7 +818,7 @@ struct VSel {
 #pragma unroll
         for (int j = 0; j < (int)(kOneWave / 64); ++j) vset(j, seg[64 * j + lane]);
         const uint32_t mbb = (uint32_t)(uintptr_t)mb;
-        while (lr - fr > 3 && depth > 0) {
+        while (lr - fr > 64 && depth > 0) {  // (<= 64 positions: the one-row rounds below)
             --depth;
             ++nrounds;
             const uint32_t A = fr + 1, B = fr + (lr - fr) / 2, C = lr - 1;
@@ -893,8 +911,71 @@ struct VSel {
         }
 #pragma unroll
         for (int j = 0; j < (int)(kOneWave / 64); ++j) seg[64 * j + lane] = vget(j);
+        if (lr - fr > 3 && depth > 0) row_rounds(seg, reinterpret_cast<uint32_t*>(mb), f0, fr, lr, nrounds);
         f = f0 + fr;
         l = f0 + lr;
+    }
+    // Rounds of <= 64 positions on one register pair (wave 0): lane i holds position f0 + w + i (w = fr at entry)
+    // and [a, b) is the segment in lanes.  Masks are ballots, ranks mbcnt, Ks the crossing over the 64 split
+    // points, and the swaps L_k <-> R_k one lane permutation: each swapping lane finds its partner's lane in a
+    // 64-entry table in the mailbox (written by the partners, read by the same wave in program order) and takes
+    // its value by ds_bpermute.  No position is both a swapping GE and a swapping LE (L_k < R_k for k <= Ks), so
+    // every lane has at most one partner.  Then the lanes go back to seg.
+    __device__ __forceinline__ void row_rounds(double* seg, uint32_t* tab, uint32_t f0, uint32_t& fr, uint32_t& lr,
+                                               uint32_t& nrounds) {
+        const uint32_t me = (uint32_t)lane, w = fr, n0 = lr - fr;
+        const uint32_t nr = nth - f0 - w;  // nth in lanes (inside [0, n0))
+        double x = seg[w + me];            // (lanes past n0 read the slots after: never live)
+        uint32_t a = 0, b = n0;
+        while (b - a > 3 && depth > 0) {
+            --depth;
+            ++nrounds;
+            const uint32_t A = a + 1, B = a + (b - a) / 2, C = b - 1;
+            const double va = uni(lane_read(x, (int)A)), vb = uni(lane_read(x, (int)B)), vc = uni(lane_read(x, (int)C));
+            const double x0 = uni(lane_read(x, (int)a));
+            uint32_t ch;
+            double pe;
+            median3(va, vb, vc, A, B, C, ch, pe);
+            x = me == a ? pe : (me == ch ? x0 : x);  // std::iter_swap(first, chosen)
+            const bool live = me >= a && me < b;
+            const uint64_t ge = __ballot(live && me != a && !(x < pe)), le = __ballot(live && !(pe < x));
+            const uint32_t tG = popc(ge), tL = popc(le);
+            const uint32_t ks = uni(wave_crossing_ks(0u, tL, ge, le));
+            const uint32_t lk1 = ks + 1u <= tG ? uni(wave_select_bit(ge, ks)) : kNone;
+            const uint32_t rk = ks >= 1u ? uni(wave_select_bit(le, tL - ks)) : kNone;
+            const uint32_t cut = lk1 < rk ? lk1 : rk;
+            if (cut == nr && !rec && nth >= 1u) {  // vec[nth - 1] after this round (pre-swap values, see block_round)
+                const uint32_t lk = ks >= 1u ? uni(wave_select_bit(ge, ks - 1u)) : kNone;
+                lo_val = uni(lane_read(x, (int)(lk == cut - 1u ? rk : cut - 1u)));
+                rec = true;
+            }
+            if (ks) {
+                // GE rank k (from the left) <-> LE rank k (from the right), k <= Ks
+                const uint32_t kg = lanes_below(ge) + 1u, kl = tL - lanes_below(le);
+                const bool sg = ((ge >> me) & 1ull) && kg <= ks, sl = ((le >> me) & 1ull) && kl <= ks;
+                if (sl) tab[kl - 1u] = me;
+                if (sg) tab[64u + kg - 1u] = me;
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t partner = sg ? tab[kg - 1u] : (sl ? tab[64u + kl - 1u] : me);
+                const uint64_t u = __builtin_bit_cast(uint64_t, x);
+                const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(partner * 4u), (int)(uint32_t)u);
+                const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(partner * 4u), (int)(uint32_t)(u >> 32));
+                x = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (dg && dg->tr) {
+                double* const v = trace_rec(1, f0 + w + a, f0 + w + b, pe, ks, tG, tL, f0 + w + cut);
+                if (v) {
+                    if (me < n0) v[f0 + w + me] = x;
+                    if (me == 0) ++dg->ntr;
+                }
+            }
+            if (cut <= nr) a = cut;
+            else b = cut;
+        }
+        if (me < n0) seg[w + me] = x;
+        fr = w + a;
+        lr = w + b;
     }
     // ------------------------------------------------------------------ std::nth_element(vec, vec + nth)
     // (vec[nth - 1], vec[nth]) of the post-state, on thread 0

@@ -17,7 +17,9 @@ Every struct holds
 
 The asm blocks carry their own wait states (hipcc pads none inside a block): a VALU write of VCC read as a constant
 by the next VALU needs one (cls4 orders its compares for it), a VALU write of a VGPR read by v_readlane needs one
-(w1src / w1tgt open with s_nop 0; the exchange quads' readlanes come after four compares).
+(w1src / w1tgt open with s_nop 0; the exchange quads' readlanes come after four compares), and a VALU write of an
+SGPR read by a buffer load needs five (load opens with s_nop 4: its descriptor may come straight from
+v_readfirstlane).
   src4<Q, S>(p, pb) / src4e<Q, S>(p, pb, ra, len)   the sources of an exchange write the mailbox   (side S)
   tgt4<Q, S>(p, pb) / tgt4e<Q, S>(p, pb, ra, len)   the targets take the mailbox values            (side S)
                                       (the e forms test each row against the row range [ra, ra + len])
@@ -63,7 +65,9 @@ class Gen:
     # ---------------------------------------------------------------- whole-vector blocks (inside the struct)
     def members(self):
         B, n = self.base, self.rows
-        load = []
+        # s_nop 4 first: the descriptor's SGPRs may come straight from v_readfirstlane, and a VALU write of an SGPR
+        # read by a VMEM instruction needs five wait states (hipcc pads none inside the block)
+        load = ["s_nop 4"]
         for r in range(n):
             load += [f"v_add_u32 %[vt], 0x{r * 0x1000:x}, %[vo]",
                      f"buffer_load_dwordx2 {self.reg(r)}, %[vt], %[rs], 0 offen ;@vfix 0"]
