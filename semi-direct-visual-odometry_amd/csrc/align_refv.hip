@@ -635,6 +635,9 @@ struct VSel {
     template <bool kWrite>
     __device__ __forceinline__ void exchange(const Ctl& C, int side, uint32_t s0, uint32_t s1, uint32_t bstep, double p,
                                              uint32_t k0, uint32_t k1, bool chunked) {
+        // (fresh opaque copies: the compiler would otherwise compute both sides' row ranges and masks for the sources
+        // and the targets up front and keep them, spilled, across the barrier)
+        asm volatile("" : "+s"(s0), "+s"(s1));
         const WaveRows w = wave_segment(s0, s1);
         if (w.rlo > w.rhi) return;
         const uint64_t gfirst = side == 0 ? w.ge_first : w.le_first;
