@@ -623,7 +623,14 @@ struct VSel {
         opaque(ra, rb);
         constexpr int r0 = 4 * kQG * Gq, r1 = r0 + 4 * (int)sizeof...(Is) - 1;
         if (r1 < ra || r0 > rb) return;
-        if (r0 >= ra && r1 <= rb) (ex_quad_in<kQG * Gq + Is, kWrite, S>(C, p, pb), ...);  // whole group inside
+        if (r0 >= ra && r1 <= rb) {  // whole group inside
+            if constexpr (!kWrite && G::kTgt8 && kQG == 4 && sizeof...(Is) == 4 && r1 < 4 * kGenQuads) {
+                G::template tgt8<2 * Gq, S>(p, pb[r0 >> 6]);  // (eight mailbox reads in flight per block)
+                G::template tgt8<2 * Gq + 1, S>(p, pb[r0 >> 6]);
+            } else {
+                (ex_quad_in<kQG * Gq + Is, kWrite, S>(C, p, pb), ...);
+            }
+        }
         else (ex_quad<kQG * Gq + Is, kWrite, S>(C, p, ra, rb, pb), ...);
     }
     template <bool kWrite, int S, int... Gs>

@@ -81,6 +81,7 @@ class Gen:
         return f'''    static constexpr int kBase = {B};       // first data VGPR
     static constexpr int kRegRows = {n};    // rows in v{B}..v255
     static constexpr int kGenQuads = {n // 4};   // register quads with generated bodies (rows 0 .. {4 * (n // 4) - 1})
+    static constexpr bool kTgt8 = {"true" if self.name == "RowsA" else "false"};  // tgt8: eight target rows per block
     static __device__ __forceinline__ void fence() {{ asm volatile(";@vfence {B}"); }}
     // rows 0..{n - 1} of src (positions 512 r + tid) into the data registers; lanes past `bytes` read 0 (buffer range)
     static __device__ __forceinline__ void load(const double* src, uint32_t bytes, int tid) {{
@@ -153,6 +154,7 @@ class Gen:
     template <int Q> static __device__ __forceinline__ void cls4(double p, uint32_t (&acc)[4]);
     template <int Q, int S> static __device__ __forceinline__ void src4(double p, uint32_t pb);
     template <int Q, int S> static __device__ __forceinline__ void tgt4(double p, uint32_t pb);
+    template <int O, int S> static __device__ __forceinline__ void tgt8(double p, uint32_t pb);
     template <int Q, int S> static __device__ __forceinline__ void src4e(double p, uint32_t pb, uint32_t ra, uint32_t len);
     template <int Q, int S> static __device__ __forceinline__ void tgt4e(double p, uint32_t pb, uint32_t ra, uint32_t len);
     template <int Q, int S> static __device__ __forceinline__ void w1src(uint32_t ml, uint32_t mh, uint32_t pre, uint32_t ks,
@@ -178,8 +180,8 @@ class Gen:
                 f"[a2] \"+v\"(acc[2]), [a3] \"+v\"(acc[3]), [m] \"=&s\"(m)\n                 : [p] \"s\"(p)\n"
                 f"                 : \"vcc\");\n}}\n")
 
-    def exch(self, q, side, write, edge):
-        rows = list(range(4 * q, 4 * q + 4))
+    def exch(self, q, side, write, edge, nr=4):
+        rows = list(range(nr * q, nr * q + nr))
         cmp = "v_cmp_nlt_f64" if side == 0 else "v_cmp_ngt_f64"
         L = ["s_mov_b64 %[sv], exec"]
         L += [f"{cmp} %[m{i}], {self.reg(r)}, %[p] ;@vfix 1" for i, r in enumerate(rows)]
@@ -196,14 +198,14 @@ class Gen:
             for i, r in enumerate(rows):
                 L += [f"s_mov_b64 exec, %[m{i}]", f"v_mov_b64 {self.reg(r)}, %[t{i}] ;@vfix 0"]
         L.append("s_mov_b64 exec, %[sv]")
-        outs = ['[m0] "=&s"(m0)', '[m1] "=&s"(m1)', '[m2] "=&s"(m2)', '[m3] "=&s"(m3)', '[sv] "=&s"(sv)',
-                '[t] "=&s"(t)', '[k] "=&v"(k)', '[a] "=&v"(a)']
-        decl = "uint64_t m0, m1, m2, m3, sv;\n    uint32_t t, k, a;\n"
+        outs = [f'[m{i}] "=&s"(m{i})' for i in range(nr)] + ['[sv] "=&s"(sv)', '[t] "=&s"(t)', '[k] "=&v"(k)',
+                                                              '[a] "=&v"(a)']
+        decl = "uint64_t " + ", ".join(f"m{i}" for i in range(nr)) + ", sv;\n    uint32_t t, k, a;\n"
         if not write:
-            outs += [f'[t{i}] "=&v"(t{i})' for i in range(4)]
-            decl += "    uint64_t t0, t1, t2, t3;\n"
+            outs += [f'[t{i}] "=&v"(t{i})' for i in range(nr)]
+            decl += "    uint64_t " + ", ".join(f"t{i}" for i in range(nr)) + ";\n"
         ins = ['[p] "s"(p)', '[pb] "v"(pb)'] + (['[ra] "s"(ra)', '[len] "s"(len)'] if edge else [])
-        name = ("src4" if write else "tgt4") + ("e" if edge else "")
+        name = ("src" if write else "tgt") + str(nr) + ("e" if edge else "")
         args = "double p, uint32_t pb" + (", uint32_t ra, uint32_t len" if edge else "")
         return (f"template <> __device__ __forceinline__ void {self.name}::{name}<{q}, {side}>({args}) {{\n    {decl}"
                 f"    asm volatile(\"{asm(L)}\"\n                 : {', '.join(outs)}\n                 : {', '.join(ins)}\n"
@@ -249,6 +251,10 @@ class Gen:
                 for e in (False, True):
                     out.append(self.exch(q, s, True, e))
                     out.append(self.exch(q, s, False, e))
+        if self.name == "RowsA":  # (targets of a wholly covered quad pair: eight reads in flight; LayA has the registers)
+            for o in range(self.rows // 8):
+                for s in (0, 1):
+                    out.append(self.exch(o, s, False, False, nr=8))
         for q in range(2):
             for s in (0, 1):
                 out.append(self.w1quad(q, s, True))
