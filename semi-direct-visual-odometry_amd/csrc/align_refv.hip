@@ -965,13 +965,15 @@ struct VSel {
                 const bool sg = ((ge >> me) & 1ull) && kg <= ks, sl = ((le >> me) & 1ull) && kl <= ks;
                 if (sl) tab[kl - 1u] = me;
                 if (sg) tab[64u + kg - 1u] = me;
-                __builtin_amdgcn_wave_barrier();
+                // (the table entries come from other lanes: a compiler memory barrier keeps the loads after the
+                // stores; the LDS keeps one wave's accesses in order)
+                asm volatile("" ::: "memory");
                 const uint32_t partner = sg ? tab[kg - 1u] : (sl ? tab[64u + kl - 1u] : me);
                 const uint64_t u = __builtin_bit_cast(uint64_t, x);
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(partner * 4u), (int)(uint32_t)u);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(partner * 4u), (int)(uint32_t)(u >> 32));
                 x = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
             }
             if (dg && dg->tr) {
                 double* const v = trace_rec(1, f0 + w + a, f0 + w + b, pe, ks, tG, tL, f0 + w + cut);
