@@ -197,6 +197,13 @@ class ImagePyramid:
         self.set = None
 
 
+def _frozen(v):
+    """A read-only float64 copy of v (the per-frame SoA caches rely on positions changing only by assignment)."""
+    a = np.array(v, dtype=np.float64)
+    a.flags.writeable = False
+    return a
+
+
 class PointType:  # Point::PointType (include/point.hpp:18-24)
     GOOD, DELETED, CANDIDATE, UNKNOWN = 0, 1, 2, 3
 
@@ -207,7 +214,7 @@ class Point:
     NO_FRAME = 2 ** 64 - 1  # m_lastProjectedKFId(-1) on a uint64
 
     def __init__(self, position):
-        self.position = position
+        self._position = _frozen(position)  # (a new point is in no frame's cached arrays yet: no version bump)
         self.type = PointType.UNKNOWN
         self.features = []
         self.last_projected_kf_id = Point.NO_FRAME
@@ -220,8 +227,9 @@ class Point:
     def find_frame(self, frame):  # src/point.cpp: any observing feature in `frame`
         return any(f.frame is frame for f in self.features)
 
-    # always a float64 array (_feature_arrays joins the raw bytes).  Setting it bumps a global version that
-    # invalidates every Frame's cached point array (a point is not told which frames' features hold it).
+    # always a read-only float64 array (_feature_arrays joins the raw bytes; an in-place edit would leave the frames'
+    # cached arrays stale, so it raises instead).  Assigning it bumps a global version that invalidates every Frame's
+    # cached point array (a point is not told which frames' features hold it).
     _ver = 0
 
     @property
@@ -230,7 +238,7 @@ class Point:
 
     @position.setter
     def position(self, v):
-        self._position = np.asarray(v, dtype=np.float64)
+        self._position = _frozen(v)
         Point._ver += 1
 
 
@@ -252,20 +260,30 @@ class Feature:
         self.point = point
 
     def _touch(self):  # the owning frame's cached feature arrays are stale
-        fr = getattr(self, "frame", None)
+        fr = getattr(self, "_frame", None)
         cell = getattr(fr, "_feat_ver", None)
         if cell is not None:
             cell[0] += 1
 
-    # always a float64 array (_feature_arrays joins the raw bytes); assignments (not in-place edits of the array)
-    # invalidate the frame's cached arrays
+    @property
+    def frame(self):
+        return self._frame
+
+    @frame.setter
+    def frame(self, fr):  # both the old and the new frame's cached arrays are stale
+        self._touch()
+        self._frame = fr
+        self._touch()
+
+    # always a read-only float64 array (_feature_arrays joins the raw bytes); assignments invalidate the frame's
+    # cached arrays, in-place edits raise (they would leave the cache stale)
     @property
     def pixel_position(self):
         return self._px
 
     @pixel_position.setter
     def pixel_position(self, v):
-        self._px = np.asarray(v, dtype=np.float64)
+        self._px = _frozen(v)
         self._touch()
 
     @property

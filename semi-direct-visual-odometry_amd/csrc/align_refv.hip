@@ -68,6 +68,8 @@ struct Lay {
     static_assert(R > G::kRegRows && R <= kRowPad, "rows");
     static_assert(2 * kOneWave <= MB && MB % 64 == 0, "one-wave segment and its mailbox");
     static_assert(!PRE || kStage + 64 * G::kRegRows <= MB, "staging of wave 0's rows inside the mailbox");
+    // stage_wave0: waves 1..7 take rows wave - 1 + 7 i, i < R / 7, which reaches every row only for R a multiple of 7
+    static_assert(!PRE || R % (kVW - 1) == 0, "stage_wave0 covers every row");
 };
 using LayA = Lay<RowsA, 98, 12288, true>;   // 50 176 slots: 88 register rows (v80..v255) + 10 LDS rows
 using LayB = Lay<RowsB, 118, 4352, false>;  // 60 416 slots: 92 register rows (v72..v255) + 26 LDS rows

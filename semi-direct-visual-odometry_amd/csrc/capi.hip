@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -83,6 +84,9 @@ struct svo_ctx {
     // every other user of the block first drains them (ctx_pinned)
     size_t ring_off = 0;
     bool ring_pending = false;
+    // pyramid sets with a build_async the context stream has not waited for yet (set_join removes them); the
+    // batches' runs join the sets their pairs read from this list (a batch never dereferences a set it keeps)
+    std::vector<svo_pyramid_set*> pending_sets;
 };
 
 // at least `bytes` of the context's scratch (the previous contents are not kept)
@@ -185,12 +189,31 @@ struct svo_pyramid_set {
     bool pending = false;        // a build_async whose `ready` the context stream has not waited for yet
 };
 
-// the context stream waits for the set's last asynchronous build (every user of a set's planes on the context
-// stream goes through this first: uploads, builds, downloads, and the batches' set_pair / set_pairs)
-static hipError_t set_join(svo_pyramid_set* p) {
+// the context stream waits for the set's last asynchronous build.  Every user of a set's planes on the context
+// stream goes through this first: uploads, builds, downloads, the batches' set_pair / set_pairs and runs
+// (join_pending), FeatureAlignment, the depth filter and feature detection / selection.
+static void pending_remove(svo_ctx* c, const svo_pyramid_set* p) {
+    auto& v = c->pending_sets;
+    v.erase(std::remove(v.begin(), v.end(), p), v.end());
+}
+static hipError_t set_join(const svo_pyramid_set* cp) {
+    svo_pyramid_set* p = const_cast<svo_pyramid_set*>(cp);
     if (!p || !p->pending) return hipSuccess;
     p->pending = false;
-    return hipStreamWaitEvent(p->ctx->stream, p->ready, 0);
+    pending_remove(p->ctx, p);
+    hipError_t e = hipSetDevice(p->ctx->device);
+    if (e == hipSuccess) e = hipStreamWaitEvent(p->ctx->stream, p->ready, 0);
+    return e;
+}
+// the sets among `sets` that still have a pending asynchronous build (matched by address against the context's
+// list, so a set destroyed since it was recorded is never touched)
+static hipError_t join_pending(svo_ctx* c, const std::vector<const svo_pyramid_set*>& sets) {
+    for (const svo_pyramid_set* q : sets) {
+        if (std::find(c->pending_sets.begin(), c->pending_sets.end(), q) == c->pending_sets.end()) continue;
+        const hipError_t e = set_join(q);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 struct svo_align_batch {
@@ -219,7 +242,17 @@ struct svo_align_batch {
     bool ran;
     uint8_t* d_stage = nullptr;  // svo_align_batch_set_pairs: packed features + row offsets (grow-only)
     size_t stage_bytes = 0;
+    // per pair the ref / lastKF / cur sets its planes come from (run joins their pending builds)
+    std::vector<std::array<const svo_pyramid_set*, 3>> pair_sets;
 };
+// the distinct sets the batch's pairs read now
+static std::vector<const svo_pyramid_set*> batch_sets(const svo_align_batch* b) {
+    std::vector<const svo_pyramid_set*> v;
+    for (const auto& t : b->pair_sets)
+        for (const svo_pyramid_set* p : t)
+            if (p && std::find(v.begin(), v.end(), p) == v.end()) v.push_back(p);
+    return v;
+}
 
 extern "C" {
 
@@ -356,6 +389,7 @@ int svo_pyramid_set_destroy(svo_pyramid_set* p) {
         (void)hipStreamSynchronize(p->ctx->prep);
         (void)hipEventDestroy(p->ready);
     }
+    pending_remove(p->ctx, p);
     (void)hipFree(p->d_base);
     delete p;
     return SVO_OK;
@@ -406,6 +440,7 @@ int svo_pyramid_set_build_async(svo_pyramid_set* p, int32_t first, int32_t count
     SVO_HIP(hipGetLastError());
     SVO_HIP(hipEventRecord(p->ready, c->prep));
     p->pending = true;
+    if (std::find(c->pending_sets.begin(), c->pending_sets.end(), p) == c->pending_sets.end()) c->pending_sets.push_back(p);
     return SVO_OK;
 }
 
@@ -413,7 +448,7 @@ int svo_pyramid_set_download(const svo_pyramid_set* p, int32_t frame, int32_t le
     if (!p || !out) return fail(SVO_ERR_ARG, "null argument");
     if (frame < 0 || frame >= p->n_frames || level < 0 || level >= p->levels) return fail(SVO_ERR_ARG, "index out of range");
     SVO_HIP(hipSetDevice(p->ctx->device));
-    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(p)));
+    SVO_HIP(set_join(p));
     const uint8_t* src = p->d_base + (size_t)frame * p->stride + (gradient ? p->grad_off : 0) + p->geom.off[level];
     SVO_HIP(hipMemcpyAsync(out, src, (size_t)p->geom.w[level] * p->geom.h[level], hipMemcpyDeviceToHost, p->ctx->stream));
     SVO_HIP(hipStreamSynchronize(p->ctx->stream));
@@ -462,6 +497,7 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
     b->geom = make_geom(cam->width, cam->height, prm->max_level + 1);
     b->h_pairs.assign(n_pairs, svo::PairDesc{});
     b->pair_set.assign(n_pairs, 0);
+    b->pair_sets.assign(n_pairs, {nullptr, nullptr, nullptr});
     const size_t F = (size_t)n_pairs * max_features;
     hipError_t e = hipSuccess;
 #define ALLOC(ptr, bytes) if (e == hipSuccess) e = hipMalloc(&ptr, bytes)
@@ -552,9 +588,10 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
     if ((rc = check_frame(b, kf_set, kf_frame)) != SVO_OK) return rc;
     if ((rc = check_frame(b, cur_set, cur_frame)) != SVO_OK) return rc;
     SVO_HIP(hipSetDevice(b->ctx->device));
-    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(ref_set)));
-    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(kf_set)));
-    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(cur_set)));
+    SVO_HIP(set_join(ref_set));
+    SVO_HIP(set_join(kf_set));
+    SVO_HIP(set_join(cur_set));
+    b->pair_sets[pair] = {ref_set, kf_set, cur_set};
     svo::PairDesc& d = b->h_pairs[pair];
     d.ref_pyr = ref_set->d_base + (size_t)ref_frame * ref_set->stride;
     d.kf_pyr = kf_set->d_base + (size_t)kf_frame * kf_set->stride;
@@ -652,9 +689,10 @@ int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, 
     const int64_t T = off[count];
     if (T > 0 && (!px || !bearing || !point || !has_point)) return fail(SVO_ERR_ARG, "null feature array");
     SVO_HIP(hipSetDevice(b->ctx->device));
-    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(ref_set)));
-    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(kf_set)));
-    SVO_HIP(set_join(const_cast<svo_pyramid_set*>(cur_set)));
+    SVO_HIP(set_join(ref_set));
+    SVO_HIP(set_join(kf_set));
+    SVO_HIP(set_join(cur_set));
+    for (int32_t i = 0; i < count; ++i) b->pair_sets[first + i] = {ref_set, kf_set, cur_set};
     for (int32_t i = 0; i < count; ++i) {
         svo::PairDesc& d = b->h_pairs[first + i];
         d.ref_pyr = ref_set->d_base + (size_t)frames[3 * i] * ref_set->stride;
@@ -770,6 +808,8 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     for (int32_t i = 0; i < b->n_pairs; ++i)
         if (!b->pair_set[i]) return fail(SVO_ERR_STATE, "pair %d was never set", i);
     SVO_HIP(hipSetDevice(b->ctx->device));
+    // a set the pairs read may have been rebuilt asynchronously since set_pair(s) (build_async after the hand-over)
+    SVO_HIP(join_pending(b->ctx, batch_sets(b)));
     svo::AlignArgs a;
     a.pairs = b->d_pairs;
     a.px = b->d_px; a.bearing = b->d_bearing; a.point = b->d_point; a.has_point = b->d_has_point;
@@ -1027,6 +1067,8 @@ int svo_feature_align(svo_ctx* c, const svo_camera* cam, int32_t patch_size, con
     if (ref_set->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
     if (ref_set->width != cam->width || ref_set->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
     if (n == 0) return SVO_OK;
+    SVO_HIP(set_join(ref_set));
+    SVO_HIP(set_join(cur_set));
     std::vector<const uint8_t*> rg(n);
     for (int32_t i = 0; i < n; ++i) {
         const int32_t f = ref_frames ? ref_frames[i] : ref_frame;
@@ -1050,7 +1092,9 @@ int svo_feature_align_multi(svo_ctx* c, const svo_camera* cam, int32_t patch_siz
         if (p->width != cam->width || p->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
         if (ref_frames[i] < 0 || ref_frames[i] >= p->n_frames) return fail(SVO_ERR_ARG, "ref frame %d out of range", ref_frames[i]);
         rg[i] = p->d_base + (size_t)ref_frames[i] * p->stride + p->grad_off;
+        SVO_HIP(set_join(p));
     }
+    SVO_HIP(set_join(cur_set));
     return feature_align_impl(c, cam, patch_size, rg, cur_set, cur_frame, n, ref_px, px_inout, err, status);
 }
 
@@ -1161,6 +1205,7 @@ int svo_depth_update(svo_ctx* c, const svo_camera* cam, int32_t n_kf, const svo_
         if (p->ctx != c) return fail(SVO_ERR_ARG, "pyramid set belongs to another context");
         if (p->width != cam->width || p->height != cam->height) return fail(SVO_ERR_ARG, "camera/pyramid size mismatch");
         if (frame < 0 || frame >= p->n_frames) return fail(SVO_ERR_ARG, "frame %d out of range", frame);
+        SVO_HIP(set_join(p));
         return SVO_OK;
     };
     int rc;
@@ -1255,6 +1300,7 @@ static int fs_check(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t
     if (frame < 0 || frame >= p->n_frames) return fail(SVO_ERR_ARG, "frame %d out of range", frame);
     if (threshold < 0) return fail(SVO_ERR_ARG, "threshold < 0");
     if ((int64_t)p->width * p->height >= ((int64_t)1 << 24)) return fail(SVO_ERR_ARG, "image of 2^24 pixels or more");
+    SVO_HIP(set_join(p));
     return SVO_OK;
 }
 

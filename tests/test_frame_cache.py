@@ -89,3 +89,30 @@ def test_rows_rejects_mixed_dtypes():
     reinterpreted."""
     vals = [np.array([1.0, 2.0]), np.array([3, 4], np.int64)]
     assert np.array_equal(core._rows(vals, 2), [[1.0, 2.0], [3.0, 4.0]])
+
+
+def test_positions_read_only_and_point_construction_keeps_caches():
+    """in-place edits of a cached position raise instead of leaving the cache stale; constructing a
+    Point (in no frame yet) does not invalidate other frames' cached point arrays; reassigning Feature.frame
+    invalidates both frames."""
+    import pytest
+    fr, other = _frame(), _frame()
+    p = svo_amd.Point([1.0, 2.0, 3.0])
+    f = svo_amd.Feature(fr, np.array([10.0, 20.0]), point=p)
+    fr.add_feature(f)
+    with pytest.raises(ValueError):
+        f.pixel_position[0] = 5.0
+    with pytest.raises(ValueError):
+        p.position += 1.0
+    src = np.array([1.0, 1.0])
+    g = svo_amd.Feature(fr, src)
+    assert src.flags.writeable  # the caller's array is copied, not frozen
+    fr.add_feature(g)
+    a = fr.feature_arrays()
+    svo_amd.Point([4.0, 5.0, 6.0])  # a new point: no frame holds it
+    assert fr.feature_arrays()[2] is a[2]
+    other.add_feature(g)
+    b = other.feature_arrays()
+    g.frame = other
+    assert fr.feature_arrays()[0] is not a[0] and other.feature_arrays()[0] is not b[0]
+    assert _same([fr]) and _same([other])

@@ -8,6 +8,8 @@ Tolerances:
   * final pose vs the reference semantics (libstdc++ nth_element) .. 1e-5 (north_star tolerance)
   * FeatureAlignment (px, err, status) ........................... bit-exact
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -15,6 +17,7 @@ import oracle as O
 import svo_amd
 import svo_amd.synth as synth
 from common import canon, gpu_batch, make_pairs, oracle_align
+from svo_amd._capi import check, lib
 
 pytestmark = pytest.mark.gpu
 
@@ -296,3 +299,76 @@ def test_pyramid_build_async_pipeline():
     b.run()
     pc, _, _ = b.results()
     assert np.array_equal(pa, pc)
+
+
+def test_build_async_consumers_wait_for_the_rebuild():
+    """Every consumer of a set's planes waits for the set's pending svo_pyramid_set_build_async: the set
+    first holds scene X's pyramids, then scene Y's base images are uploaded and rebuilt asynchronously, and the
+    consumer is called straight away.  A consumer that did not wait would read X's (or half-built) gradient /
+    levels.  The set is large (384 frames, ~0.3 ms of build) and the frames read are the last ones built, so a
+    missing wait shows.  Consumers: FeatureAlignment, feature detection, an alignment batch whose pairs were set
+    before the rebuild (run joins it), and FeatureAlignment through a multi-set call."""
+    sx, sy = synth.make_pair(seed=synth.SEED_BASE + 3), synth.make_pair(seed=synth.SEED_BASE + 9)
+    N, W, H, L = 384, 1241, 376, 5
+    frames_of = lambda s: np.stack([s.ref_img, s.kf_img, s.cur_img] * (N // 3))
+    X, Y = frames_of(sx), frames_of(sy)
+    cam = svo_amd.PinholeCamera.kitti()
+    ps = svo_amd.PyramidSet(N, W, H, L)
+    ps.upload(0, X)
+    ps.build()
+    fr_ref, fr_kf, fr_cur = N - 3, N - 2, N - 1
+
+    def rebuild(imgs):
+        ps.upload(0, imgs)
+        ps.build_async()
+
+    # FeatureAlignment on Y's gradients
+    rng = np.random.default_rng(5)
+    ref_px = sy.px[:1500].copy()
+    init = ref_px + rng.uniform(-1.5, 1.5, ref_px.shape)
+    gy_ref, gy_cur = O.build_pyramid(sy.ref_img, 1)[1], O.build_pyramid(sy.cur_img, 1)[1]
+    px_c, err_c, st_c = O.feature_align(sy.camera, 7, gy_ref, gy_cur, ref_px, init)
+    rebuild(Y)
+    px_g = init.copy()
+    svo_amd.FeatureAlignment(7).align_batch(ps, fr_ref, ps, fr_cur, ref_px, px_g, cam)
+    assert np.array_equal(px_g, px_c)
+    # feature detection on X's level-0 gradient (keys response << 24 | y * W + x, row-major)
+    gx_cur = O.build_pyramid(sx.cur_img, 1)[1][:W * H]
+    thr = 50
+    idx = np.nonzero(gx_cur > thr)[0].astype(np.uint32)
+    keys_c = (gx_cur[idx].astype(np.uint32) << 24) | idx
+    rebuild(X)
+    fs = svo_amd.FeatureSelection(W, H, 30)
+    keys = np.zeros(W * H, np.uint32)
+    n = ctypes.c_int32()
+    check(lib().svo_feature_detect(fs.ctx.handle, ps.handle, fr_cur, thr, W * H,
+                                                          keys.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n)))
+    assert np.array_equal(keys[:n.value], keys_c)
+    # an alignment batch handed Y's pair while the set still holds X, then the set rebuilt with Y: run waits
+    b = svo_amd.AlignBatch(cam, 5, 0, L - 1, 1, 2000, median_mode=svo_amd.MEDIAN_REFERENCE)
+    frames = np.array([[fr_ref, fr_kf, fr_cur]], np.int32)
+    poses = np.concatenate([sy.ref_pose, sy.kf_pose, sy.cur_init_pose])[None]
+    b.set_pairs(0, ps, ps, ps, frames, poses, np.array([[sy.n_ref, sy.n_kf]], np.int32), sy.px, sy.bearing, sy.point,
+                sy.has_point)
+    rebuild(Y)
+    b.run()
+    pg, eg, sg = b.results()
+    pc, ec, stc, _ = oracle_align(sy, 5, 0, L - 1, mode=0)
+    assert np.abs(canon(pg[0]) - canon(pc)).max() <= 1e-9 and sg[0] == stc
+    # FeatureAlignment with per-candidate sets (svo_feature_align_multi) after a rebuild with X
+    gx_ref = O.build_pyramid(sx.ref_img, 1)[1]
+    gx_cur2 = O.build_pyramid(sx.cur_img, 1)[1]
+    ref_px = sx.px[:1000].copy()
+    init = ref_px + rng.uniform(-1.5, 1.5, ref_px.shape)
+    px_c, _, _ = O.feature_align(sx.camera, 7, gx_ref, gx_cur2, ref_px, init)
+    rebuild(X)
+    px_g = np.ascontiguousarray(init.copy())
+    err = np.zeros(len(ref_px))
+    st = np.zeros(len(ref_px), np.int32)
+    sets = (ctypes.c_void_p * len(ref_px))(*([ps.handle] * len(ref_px)))
+    rf = np.full(len(ref_px), fr_ref, np.int32)
+    check(lib().svo_feature_align_multi(
+        ps.ctx.handle, ctypes.byref(cam.as_c()), 7, sets, rf.ctypes.data_as(ctypes.c_void_p), ps.handle, fr_cur,
+        len(ref_px), np.ascontiguousarray(ref_px).ctypes.data_as(ctypes.c_void_p), px_g.ctypes.data_as(ctypes.c_void_p),
+        err.ctypes.data_as(ctypes.c_void_p), st.ctypes.data_as(ctypes.c_void_p)))
+    assert np.array_equal(px_g, px_c)

@@ -39,7 +39,8 @@ Every instruction that names a fixed data register carries a `;@vfix i[,j]` tag 
 tools/check_vreg_fence.py exempts exactly those operands from the kernel's fence and requires every other operand
 below it.
 
-usage: python3 tools/gen_refv_rows.py  (writes the header; the Makefile does not run it, the output is committed)
+usage: python3 tools/gen_refv_rows.py [out]  (writes the header; the output is committed, and
+       tests/test_asm_checks.py regenerates it and fails on any difference)
 """
 import os
 
@@ -262,7 +263,7 @@ class Gen:
         return out
 
 
-def main():
+def main(out=OUT):
     parts = ["// refv_rows.h -- GENERATED by tools/gen_refv_rows.py; do not edit.",
              "// K2V's asm on its fixed data registers, one struct per register layout (see the generator's docstring).",
              "// Included inside align_refv.hip's namespace.", "#pragma once", ""]
@@ -271,10 +272,12 @@ def main():
         parts.append(f"struct {g.name} {{\n{g.members()}}};\n")
     for g in gens:
         parts += g.specializations()
-    with open(OUT, "w") as f:
+    with open(out, "w") as f:
         f.write("\n".join(parts))
-    print("wrote", OUT)
+    print("wrote", out)
 
 
 if __name__ == "__main__":
-    main()
+    # (an explicit path writes there instead: tests/test_asm_checks.py regenerates the header and diffs it)
+    import sys
+    main(sys.argv[1] if len(sys.argv) > 1 else OUT)
