@@ -208,18 +208,63 @@ class PointType:  # Point::PointType (include/point.hpp:18-24)
     GOOD, DELETED, CANDIDATE, UNKNOWN = 0, 1, 2, 3
 
 
+class _PointTable:
+    """The state of every live Point as arrays (position, type, m_lastProjectedKFId, the projection counters), one
+    row per point: Map.reproject_map gathers these fields of ~2000 points and writes the projection ids back as
+    array operations instead of walking the objects.  Rows of collected points are reused."""
+
+    def __init__(self, cap=4096):
+        self.pos = np.zeros((cap, 3))
+        self.type = np.zeros(cap, np.uint32)
+        self.last = np.zeros(cap, np.uint64)
+        self.succ = np.zeros(cap, np.int64)
+        self.fail = np.zeros(cap, np.int64)
+        self.n = 0
+        self.free = []
+
+    def alloc(self):
+        if self.free:
+            return self.free.pop()
+        if self.n == len(self.type):
+            for k in ("pos", "type", "last", "succ", "fail"):
+                a = getattr(self, k)
+                b = np.zeros((2 * len(a),) + a.shape[1:], a.dtype)
+                b[:len(a)] = a
+                setattr(self, k, b)
+        self.n += 1
+        return self.n - 1
+
+
+_PT = _PointTable()
+
+
 class Point:
     """Point(position) (src/point.cpp:6-18): position, type, the observing features and the
-    reprojection bookkeeping the Map reads (include/point.hpp:28-40)."""
+    reprojection bookkeeping the Map reads (include/point.hpp:28-40).  The fields live in a row of _PT."""
     NO_FRAME = 2 ** 64 - 1  # m_lastProjectedKFId(-1) on a uint64
 
     def __init__(self, position):
-        self._position = _frozen(position)  # (a new point is in no frame's cached arrays yet: no version bump)
-        self.type = PointType.UNKNOWN
+        i = _PT.alloc()
+        self._i = i
+        _PT.pos[i] = np.asarray(position, np.float64).reshape(3)  # (a new point is in no frame's cached arrays yet)
+        _PT.type[i] = PointType.UNKNOWN
+        _PT.last[i] = Point.NO_FRAME
+        _PT.succ[i] = 0
+        _PT.fail[i] = 0
         self.features = []
-        self.last_projected_kf_id = Point.NO_FRAME
-        self.failed_projection = 0
-        self.succeeded_projection = 0
+
+    def __del__(self):
+        try:
+            _PT.free.append(self._i)
+        except Exception:  # (interpreter shutdown)
+            pass
+
+    type = property(lambda self: int(_PT.type[self._i]), lambda self, v: _PT.type.__setitem__(self._i, v))
+    last_projected_kf_id = property(lambda self: int(_PT.last[self._i]),
+                                    lambda self, v: _PT.last.__setitem__(self._i, v))
+    succeeded_projection = property(lambda self: int(_PT.succ[self._i]),
+                                    lambda self, v: _PT.succ.__setitem__(self._i, v))
+    failed_projection = property(lambda self: int(_PT.fail[self._i]), lambda self, v: _PT.fail.__setitem__(self._i, v))
 
     def add_feature(self, feature):  # src/point.cpp:35-38
         self.features.append(feature)
@@ -227,18 +272,18 @@ class Point:
     def find_frame(self, frame):  # src/point.cpp: any observing feature in `frame`
         return any(f.frame is frame for f in self.features)
 
-    # always a read-only float64 array (_feature_arrays joins the raw bytes; an in-place edit would leave the frames'
-    # cached arrays stale, so it raises instead).  Assigning it bumps a global version that invalidates every Frame's
-    # cached point array (a point is not told which frames' features hold it).
+    # a read-only float64 copy of the row (an in-place edit would not reach the table, so it raises instead).
+    # Assigning it bumps a global version that invalidates every Frame's cached point array (a point is not told
+    # which frames' features hold it).
     _ver = 0
 
     @property
     def position(self):
-        return self._position
+        return _frozen(_PT.pos[self._i])
 
     @position.setter
     def position(self, v):
-        self._position = _frozen(v)
+        _PT.pos[self._i] = np.asarray(v, np.float64).reshape(3)
         Point._ver += 1
 
 
@@ -250,14 +295,33 @@ class Feature:
 
     def __init__(self, frame, pixel_position, level=0, point=None, bearing=None, gradient_magnitude=1.0,
                  gradient_orientation=0.0, feature_type=EDGE):
-        self.frame = frame
-        self.pixel_position = pixel_position
+        self._frame = frame
+        self._px = _frozen(pixel_position)
         self.level = level
         self.gradient_magnitude = gradient_magnitude      # m_gradientMagnitude (src/feature.cpp:15,34)
         self.gradient_orientation = gradient_orientation  # m_gradientOrientation
         self.type = feature_type
         self._bearing = None if bearing is None else np.asarray(bearing, np.float64)
-        self.point = point
+        self._point = point
+        self._touch()
+
+    @classmethod
+    def _many(cls, frame, px, level=0, points=None, gradient_magnitude=None, feature_type=EDGE):
+        """Features at the rows of px (n, 2) on `frame` without the per-object property path (the Map and
+        FeatureSelection surfaces create hundreds per call): each pixel position is a read-only row of one frozen
+        copy of px, points / gradient magnitudes per feature (None: none / 1.0).  Not added to the frame."""
+        pxf = _frozen(px)
+        n = len(pxf)
+        pts = points if points is not None else [None] * n
+        gm = gradient_magnitude if gradient_magnitude is not None else [1.0] * n
+        out = []
+        new = object.__new__
+        for i in range(n):
+            f = new(cls)
+            f.__dict__ = {"_frame": frame, "_px": pxf[i], "level": level, "gradient_magnitude": gm[i],
+                          "gradient_orientation": 0.0, "type": feature_type, "_bearing": None, "_point": pts[i]}
+            out.append(f)
+        return out
 
     def _touch(self):  # the owning frame's cached feature arrays are stale
         fr = getattr(self, "_frame", None)
@@ -385,11 +449,11 @@ class Frame:
         key = (self._feat_ver[0], Point._ver)
         c = self._soa
         if c is None or c[0] != key:
-            if c is not None and c[0][0] == key[0]:  # only point positions moved: keep px / bearing / has_point
-                self._soa = (key, c[1], c[2], _points_of(self.features), c[4])
+            if c is not None and c[0][0] == key[0]:  # only point positions moved: regather them (same rows)
+                self._soa = (key, c[1], c[2], _gather_points(c[5]), c[4], c[5])
             else:
                 self._soa = (key, *_feature_soa(self.features))
-        return self._soa[1:]
+        return self._soa[1:5]
 
 
 def _rows(vals, width):
@@ -408,19 +472,30 @@ def _rows(vals, width):
     return np.array(vals, dtype=np.float64).reshape(n, width)
 
 
+def _point_rows(feats):
+    """The _PT rows of the features' points (-1: no point)."""
+    return np.fromiter((-1 if f._point is None else f._point._i for f in feats), np.int64, count=len(feats))
+
+
+def _gather_points(idx):
+    out = _PT.pos[np.maximum(idx, 0)]
+    out[idx < 0] = 0.0
+    return out
+
+
 def _points_of(feats):
-    z = np.zeros(3)
-    return _rows([z if f.point is None else f.point.position for f in feats], 3) if feats else np.zeros((0, 3))
+    return _gather_points(_point_rows(feats)) if feats else np.zeros((0, 3))
 
 
 def _feature_soa(feats):
+    """(px, bearing, point, has_point, point rows) of the features."""
     n = len(feats)
     if n == 0:
-        return np.zeros((0, 2)), np.zeros((0, 3)), np.zeros((0, 3)), np.zeros(0, np.uint8)
+        return np.zeros((0, 2)), np.zeros((0, 3)), np.zeros((0, 3)), np.zeros(0, np.uint8), np.zeros(0, np.int64)
     px = _rows([f.pixel_position for f in feats], 2)
     br = _rows([f.bearing_vec for f in feats], 3)
-    hp = np.fromiter((f.point is not None for f in feats), dtype=np.uint8, count=n)
-    return px, br, _points_of(feats), hp
+    idx = _point_rows(feats)
+    return px, br, _gather_points(idx), (idx >= 0).astype(np.uint8), idx
 
 
 def _feature_arrays(frames):
@@ -699,18 +774,16 @@ class Map:
         kfs = [ref_frame, ref_frame.last_keyframe]
         feats = [f for kf in kfs for f in kf.features]
         off = np.cumsum([0] + [len(kf.features) for kf in kfs]).astype(np.int32)
-        index, points = {}, []
-        feat_point = np.full(max(len(feats), 1), -1, np.int32)
-        for i, f in enumerate(feats):
-            if f.point is not None:
-                k = index.setdefault(id(f.point), len(points))
-                if k == len(points):
-                    points.append(f.point)
-                feat_point[i] = k
+        # the distinct points in first-seen order (a Point hashes by identity) and each feature's index among them
+        pts = [f._point for f in feats]
+        points = list(dict.fromkeys(p for p in pts if p is not None))
+        row_of = dict(zip(points, range(len(points))))
+        feat_point = np.array([row_of.get(p, -1) for p in pts] or [-1], np.int32)
         npt = len(points)
-        pos = np.ascontiguousarray([p.position for p in points] or np.zeros((1, 3)), dtype=np.float64)
-        ptype = np.array([p.type for p in points] or [0], np.uint32)
-        plast = np.array([p.last_projected_kf_id for p in points] or [0], np.uint64)
+        prow = np.fromiter((p._i for p in points), np.int64, count=npt)
+        pos = np.ascontiguousarray(_PT.pos[prow]) if npt else np.zeros((1, 3))
+        ptype = _PT.type[prow] if npt else np.zeros(1, np.uint32)
+        plast = _PT.last[prow] if npt else np.zeros(1, np.uint64)
         n_cells = len(self.cell_orders)
         overlap = np.zeros(len(kfs), np.int32)
         sel_feat = np.zeros(n_cells, np.int32)
@@ -726,8 +799,7 @@ class Map:
                                            ptr(sel_feat), ptr(sel_cell), ptr(sel_px), ctypes.byref(m),
                                            ctypes.byref(t)))
         self.native_seconds += time.perf_counter() - t0
-        for p, last in zip(points, plast):
-            p.last_projected_kf_id = int(last)
+        _PT.last[prow] = plast[:npt]
         for k, kf in enumerate(kfs):
             overlap_keyframes.append((kf, int(overlap[k])))
         self.matches, self.trials = m.value, t.value
@@ -737,16 +809,18 @@ class Map:
         t0 = time.perf_counter()
         self.alignment.align_many(chosen, cur_frame, px)
         self.native_seconds += time.perf_counter() - t0
-        for i, ref_feature in enumerate(chosen):  # :558-569
-            point = ref_feature.point
-            point.succeeded_projection += 1
-            if point.type == PointType.UNKNOWN and point.succeeded_projection > 10:
-                point.type = PointType.GOOD
-            feature = Feature(cur_frame, px[i].copy(), 0)
-            cur_frame.add_feature(feature)
-            feature.set_point(point)
-            point.add_feature(feature)
-            self.cell_visited[sel_cell[i]] = True
+        pts = [f._point for f in chosen]
+        new = Feature._many(cur_frame, px, 0, points=pts)
+        # :558-569 (m_succeededProjection++, UNKNOWN -> GOOD past 10) on the points' rows; a point is planned at most
+        # once per call (m_lastProjectedKFId), and the end state would be the same for repeats
+        srow = np.fromiter((p._i for p in pts), np.int64, count=ns)
+        np.add.at(_PT.succ, srow, 1)
+        up = (_PT.type[srow] == PointType.UNKNOWN) & (_PT.succ[srow] > 10)
+        _PT.type[srow[up]] = PointType.GOOD
+        for point, feature in zip(pts, new):
+            point.features.append(feature)
+        cur_frame.features.extend(new)
+        self.cell_visited[sel_cell[:ns]] = True
 
     def add_new_candidate(self, feature, point, matched=False):
         point.type = PointType.CANDIDATE
@@ -755,35 +829,42 @@ class Map:
     def add_candidate_to_frame(self, frame):
         if not self.candidates:
             return
-        pos = np.array([c[1].position for c in self.candidates])
+        rows = np.fromiter((c[1]._i for c in self.candidates), np.int64, count=len(self.candidates))
+        pos = np.ascontiguousarray(_PT.pos[rows])
         t0 = time.perf_counter()
         px0 = frame.world2image(pos)
         self.native_seconds += time.perf_counter() - t0
         w, h = frame.camera.width, frame.camera.height
-        elig, cells = [], []
-        for i, q in enumerate(px0):
-            if q[0] >= 3 and q[1] >= 3 and q[0] < w - 3 and q[1] < h - 3:
-                k = self.cell_of(q)
-                if not self.cell_visited[k]:
-                    elig.append(i)
-                    cells.append(k)
+        # inside the 3-px border (isInFrame(px, 3)), cell not visited yet (:600-606); cell_of truncates like int()
+        inside = (px0[:, 0] >= 3) & (px0[:, 1] >= 3) & (px0[:, 0] < w - 3) & (px0[:, 1] < h - 3)
+        cell = np.zeros(len(px0), np.int64)
+        cell[inside] = (px0[inside, 1].astype(np.int64) // self.cell_size * self.grid_cols
+                        + px0[inside, 0].astype(np.int64) // self.cell_size)
+        elig = np.nonzero(inside)[0]
+        elig = elig[~self.cell_visited[cell[elig]]]
+        cells = cell[elig].tolist()
         px = np.ascontiguousarray(px0[elig])
-        cands = [self.candidates[i][0] for i in elig]
+        cands = [self.candidates[i][0] for i in elig.tolist()]
         t0 = time.perf_counter()
         err, _ = self.alignment.align_many(cands, frame, px)
         self.native_seconds += time.perf_counter() - t0
-        for j, i in enumerate(elig):  # the reference's order: a cell taken earlier in this loop is skipped
-            if self.cell_visited[cells[j]] or not err[j] < 50.0:
+        ok = (err < 50.0).tolist()
+        acc = []
+        for j, i in enumerate(elig.tolist()):  # the reference's order: a cell taken earlier in this loop is skipped
+            if not ok[j] or self.cell_visited[cells[j]]:
                 continue
-            feat, point = self.candidates[i][0], self.candidates[i][1]
-            feature = Feature(frame, px[j].copy(), 0)
-            frame.add_feature(feature)
-            point.add_feature(feat)
-            point.add_feature(feature)
-            feat.set_point(point)
-            feature.set_point(point)
-            self.candidates[i][2] = True
             self.cell_visited[cells[j]] = True
+            acc.append((j, i))
+        if acc:
+            pts = [self.candidates[i][1] for _, i in acc]
+            new = Feature._many(frame, px[[j for j, _ in acc]], 0, points=pts)
+            frame.features.extend(new)
+            for (_, i), point, feature in zip(acc, pts, new):
+                feat = self.candidates[i][0]
+                point.features.append(feat)
+                point.features.append(feature)
+                feat.set_point(point)
+                self.candidates[i][2] = True
         self.candidates = [c for c in self.candidates if not c[2]]  # removeMatchedCandidate
 
 
@@ -895,9 +976,8 @@ class FeatureSelection:
         self.occupancy_grid[:] = 0
 
     def _emit(self, frame, px, resp, n):
-        for i in range(n):
-            frame.add_feature(Feature(frame, px[i].copy(), 0, gradient_magnitude=float(resp[i]),
-                                      gradient_orientation=0.0, feature_type=Feature.EDGE))
+        frame.features.extend(Feature._many(frame, px[:n], 0, gradient_magnitude=resp[:n].tolist(),
+                                            feature_type=Feature.EDGE))
         return n
 
     def detect(self, frame, detection_threshold):

@@ -182,6 +182,178 @@ __global__ void __launch_bounds__(kGradThreads) abs_grad_kernel(uint8_t* stacks,
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Level-0 gradient + level 1 of BOTH stacks in one pass over the base image (pyr_l01_kernel).
+//
+// One wave streams a vertical strip of the base image down a band of level-1 rows, entirely in registers: lane l
+// holds four source columns c0 = 4 (own * strip + l - 1) .. c0 + 3 of each row as one dword (an aligned dword load
+// realigned with the right neighbour lane's dword through DPP), lanes 0 and 63 are halo lanes (their values feed
+// their neighbours' taps; they store nothing).  Per level-1 row r the wave keeps the base rows 2r-3 .. 2r+3 and
+// the gradient rows 2r-2 .. 2r+2 (Simd::AbsGradientSaturatedSum, byte-parallel; row / column neighbours by DPP);
+// the vertical [1 4 6 4 1] sums of both stacks are packed u16 pairs, the horizontal pass takes the neighbour
+// lanes' sums by DPP.  BORDER_REFLECT_101: rows through the reflected row index of each tap (every tap of a valid
+// output is one reflection away), columns by substituting the reflected sums in the edge strips.  Each output
+// row (two gradient rows of level 0, one row of each level-1 stack) leaves through the wave's 256-B LDS buffer:
+// byte writes at the row's address alignment, then aligned dword stores (the run's two partial end dwords byte by
+// byte), so every byte is written once by the wave that owns it.  Integer arithmetic only: bit-exact.
+constexpr int kL01Waves = 4;                  // independent waves per workgroup (strip x band each)
+constexpr int kL01Band = 32;                  // level-1 rows per band
+
+__device__ __forceinline__ uint32_t from_left(uint32_t v) {   // lane i <- lane i - 1 (wave_shr:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i + 1 (wave_shl:1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int refl101(int i, int n) {  // one reflection (valid taps never need two) + clamp
+    i = i < 0 ? -i : i;
+    i = i >= n ? 2 * n - 2 - i : i;
+    return min(max(i, 0), n - 1);
+}
+
+// the lane's four pixels of plane row `row` (aligned dword + the right lane's dword); lanes outside the strip's
+// loadable range read the row start (their values are never used)
+__device__ __forceinline__ uint32_t load4(const uint8_t* plane, int W, int row, int c0) {
+    const int c = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
+    const int64_t o = (int64_t)row * W + c;
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(plane + (o & ~(int64_t)3));
+    const uint32_t hi = from_right(lo);
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
+}
+
+// one output row run of a wave: lanes 1..own hold K bytes each (little-endian in v) for columns
+// col0 + K (l - 1) + i; columns in [col0, ncol) are written to dst_row (the plane row's column 0)
+template <int K>
+__device__ __forceinline__ void store_run(uint8_t* dst_row, int col0, int ncol, int own, uint32_t v, uint8_t* lbuf,
+                                          int lane) {
+    const int ch = min(col0 + K * own, ncol);
+    if (ch <= col0) return;  // (wave-uniform)
+    const uintptr_t A = reinterpret_cast<uintptr_t>(dst_row + col0);
+    const int sh = (int)(A & 3u);
+    const int n = sh + (ch - col0);
+    if (lane >= 1 && lane <= own) {
+        const int c = K * (lane - 1);
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (col0 + c + i < ch) lbuf[sh + c + i] = (uint8_t)(v >> (8 * i));
+    }
+    asm volatile("" ::: "memory");  // (the dword reads below take other lanes' bytes: in order within the wave)
+    const int lo = 4 * lane;
+    if (lo < n) {
+        const uint32_t w = reinterpret_cast<const uint32_t*>(lbuf)[lane];
+        uint8_t* g = reinterpret_cast<uint8_t*>(A & ~(uintptr_t)3) + lo;
+        if (lo >= sh && lo + 4 <= n) {
+            *reinterpret_cast<uint32_t*>(g) = w;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (lo + i >= sh && lo + i < n) g[i] = (uint8_t)(w >> (8 * i));
+        }
+    }
+    asm volatile("" ::: "memory");  // (the next run rewrites the buffer)
+}
+
+typedef uint16_t u16x2v __attribute__((ext_vector_type(2)));
+// vertical [1 4 6 4 1] sums of five rows (four pixels each): (cols 0, 2) and (cols 1, 3) as u16 pairs
+__device__ __forceinline__ void vsum5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t& ev,
+                                      uint32_t& od) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const u16x2v A = as_u16x2((a >> (8 * h)) & 0x00FF00FFu), B = as_u16x2((b >> (8 * h)) & 0x00FF00FFu);
+        const u16x2v C = as_u16x2((c >> (8 * h)) & 0x00FF00FFu), D = as_u16x2((d >> (8 * h)) & 0x00FF00FFu);
+        const u16x2v E = as_u16x2((e >> (8 * h)) & 0x00FF00FFu);
+        const u16x2v s = (A + E) + ((B + D) << (u16x2v){2, 2}) + C * (u16x2v){6, 6};
+        (h ? od : ev) = as_u32(s);
+    }
+}
+// the two level-1 pixels of the lane (columns c0 / 2, c0 / 2 + 1) from its vertical sums and its neighbours';
+// `edge` (wave-uniform): this strip holds column 0 or column W - 1 (reflected taps)
+__device__ __forceinline__ uint32_t hpass(uint32_t ev, uint32_t od, int c0, int W, bool edge) {
+    const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
+    uint32_t V[7] = {lev >> 16, lod >> 16, ev & 0xFFFFu, od & 0xFFFFu, ev >> 16, od >> 16, rev & 0xFFFFu};
+    if (edge) {  // columns c0 - 2 + j outside [0, W) take the sums of their BORDER_REFLECT_101 columns
+        if (c0 == 0) { V[0] = V[4]; V[1] = V[3]; }
+        const int d = W - 1 - c0;  // the lane's last valid offset from c0 (>= 4: no column past the edge)
+#pragma unroll
+        for (int j = 3; j < 7; ++j) {
+            // column c0 - 2 + j >= W  <=>  j >= d + 3; its reflection is V[2d + 4 - j]
+            uint32_t r = V[j];
+#pragma unroll
+            for (int k = 0; k < j; ++k) r = (j >= d + 3 && k == 2 * d + 4 - j) ? V[k] : r;
+            V[j] = r;
+        }
+    }
+    const uint32_t o0 = (V[0] + 4 * V[1] + 6 * V[2] + 4 * V[3] + V[4] + 128) >> 8;
+    const uint32_t o1 = (V[2] + 4 * V[3] + 6 * V[4] + 4 * V[5] + V[6] + 128) >> 8;
+    return o0 | (o1 << 8);
+}
+
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
+                                                                 int W, int H, int64_t off1, int W1, int H1, int own,
+                                                                 int nstrip, int nband, int first) {
+    __shared__ __attribute__((aligned(16))) uint8_t lbuf_all[kL01Waves][256];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int gw = blockIdx.x * kL01Waves + wv;
+    if (gw >= nstrip * nband) return;  // (wave-uniform)
+    const int strip = gw % nstrip, band = gw / nstrip;
+    uint8_t* const lbuf = lbuf_all[wv];
+    const int frame = first + blockIdx.y;
+    uint8_t* const ibase = stacks + frame * frame_stride;
+    uint8_t* const gbase = ibase + grad_off;
+    const int col0 = 4 * own * strip;         // the strip's first owned source column
+    const int c0 = col0 + 4 * (lane - 1);     // this lane's
+    const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
+    const bool edge = strip == 0 || col0 + 4 * own >= W;
+    // border columns of the gradient (Simd leaves them 0): byte masks of this lane
+    uint32_t colmask = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (c0 + i == 0 || c0 + i == W - 1) colmask &= ~(0xFFu << (8 * i));
+    auto row_of = [&](int y) { return refl101(y, H); };
+    auto ld = [&](int y) { return load4(ibase, W, row_of(y), c0); };
+    auto grad = [&](uint32_t up, uint32_t mid, uint32_t dn, int y) -> uint32_t {
+        const uint32_t L = from_left(mid), R = from_right(mid);
+        const uint32_t g = grad4(__builtin_amdgcn_alignbyte(mid, L, 3), __builtin_amdgcn_alignbyte(R, mid, 1), up, dn);
+        const int py = row_of(y);
+        return (py == 0 || py == H - 1) ? 0u : (g & colmask);
+    };
+    // window: R[k] = base row (logical) 2r - 3 + k, G[i] = gradient row 2r - 2 + i
+    uint32_t R[7], G[5];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) R[k] = ld(2 * r0 - 3 + k);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) G[i] = grad(R[i], R[i + 1], R[i + 2], 2 * r0 - 2 + i);
+    for (int r = r0; r < r1; ++r) {
+        // the next two base rows go out first (in flight during this row's work)
+        const uint32_t n5 = ld(2 * r + 4), n6 = ld(2 * r + 5);
+        // level-0 gradient rows 2r, 2r + 1 (this band's own source rows)
+        store_run<4>(gbase + (int64_t)(2 * r) * W, col0, W, own, G[2], lbuf, lane);
+        if (2 * r + 1 < H) store_run<4>(gbase + (int64_t)(2 * r + 1) * W, col0, W, own, G[3], lbuf, lane);
+        // level 1 of both stacks
+        uint32_t ev, od;
+        vsum5(R[1], R[2], R[3], R[4], R[5], ev, od);
+        const uint32_t oi = hpass(ev, od, c0, W, edge);
+        vsum5(G[0], G[1], G[2], G[3], G[4], ev, od);
+        const uint32_t og = hpass(ev, od, c0, W, edge);
+        store_run<2>(ibase + off1 + (int64_t)r * W1, col0 / 2, W1, own, oi, lbuf, lane);
+        store_run<2>(gbase + off1 + (int64_t)r * W1, col0 / 2, W1, own, og, lbuf, lane);
+        // advance the window by two base rows
+#pragma unroll
+        for (int k = 0; k < 5; ++k) R[k] = R[k + 2];
+        R[5] = n5;
+        R[6] = n6;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) G[i] = G[i + 2];
+        G[3] = grad(R[3], R[4], R[5], 2 * r + 3);
+        G[4] = grad(R[4], R[5], R[6], 2 * r + 4);
+    }
+}
+
+bool use_l01() {
+    static const bool old = getenv("SVO_PYR") && atoi(getenv("SVO_PYR")) == 0;  // (measurement knob, read once)
+    return !old;
+}
+
 }  // namespace
 
 // stacks: device base of the pyramid set; frame i occupies [i*stride, i*stride + 2*frame_bytes):
@@ -190,9 +362,22 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
     const int64_t grad_off = (g.frame_bytes + 255) / 256 * 256;
     const int64_t stride = (grad_off + g.frame_bytes + 255) / 256 * 256;
     const int64_t npx = (int64_t)g.w[0] * g.h[0];
-    hipLaunchKernelGGL(abs_grad_kernel, dim3((unsigned)((npx + kGradRun - 1) / kGradRun), count), dim3(kGradThreads), 0, s,
-                       stacks, stride, grad_off, g.w[0], g.h[0], first);
-    for (int l = 1; l < g.levels; ++l) {
+    int l = 1;
+    if (g.levels >= 2 && use_l01()) {
+        // strips of `own` lanes x 4 columns (<= 62 lanes: lanes 0 and 63 are halo), as few strips as the width needs
+        const int nstrip = (g.w[0] + 4 * 62 - 1) / (4 * 62);
+        const int own = (g.w[0] + 4 * nstrip - 1) / (4 * nstrip);
+        const int nband = (g.h[1] + kL01Band - 1) / kL01Band;
+        const int waves = nstrip * nband;
+        hipLaunchKernelGGL(pyr_l01_kernel, dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count),
+                           dim3(64 * kL01Waves), 0, s, stacks, stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1],
+                           own, nstrip, nband, first);
+        l = 2;
+    } else {
+        hipLaunchKernelGGL(abs_grad_kernel, dim3((unsigned)((npx + kGradRun - 1) / kGradRun), count), dim3(kGradThreads), 0,
+                           s, stacks, stride, grad_off, g.w[0], g.h[0], first);
+    }
+    for (; l < g.levels; ++l) {
         dim3 grid((g.w[l] + kDnW - 1) / kDnW, (g.h[l] + kDnH - 1) / kDnH, 2 * count);
         hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, s, stacks, stride, grad_off, g.off[l - 1], g.w[l - 1],
                            g.h[l - 1], g.off[l], g.w[l], g.h[l], first);
