@@ -85,6 +85,7 @@ struct VShared {
     double pub[6];                    // pre-values published by their owners (candidates 0-3, record 4)
     uint32_t pubk[4];                 // the candidates' target ranks (0: not a target), by their owners
     double bcd;                       // broadcast of the median between the passes
+    uint32_t srch[4];                 // (SVO_K2V_ONECHAIN) Ks, L_{Ks+1}, R_{Ks}, L_{Ks} from wave 0
     double lrow[L::kRows - L::kRegRows][kVT];  // the LDS rows of the vector (the rest is in registers)
     uint32_t tmp[2 * kVW];            // per-wave counts of the prologue
 };
@@ -96,7 +97,14 @@ struct VDiag {  // svo_debug_robust_scale diagnostics
                       // ranks, sources, barrier 2, targets, exits (dump, one-wave rounds, final), scan, crossing,
                       // searches
     uint32_t nlog;    // (stamps build) per block round: segment size and thread 0's cycles
+#if defined(SVO_STAMPS_WAVES)
+    union {
+        uint32_t log[64][2];
+        uint32_t phw[kVW][12];  // (make stamps STAMPS_WAVES=1) every wave's cycles per phase (lane 0), in place of log
+    };
+#else
     uint32_t log[64][2];
+#endif
     // round trace (svo_debug_robust_scale with out_len > 206; development): after every round a record of
     // kTrHead doubles (pass + 10 kind (0 block, 1 one-wave), f, l before the round, pivot, Ks, #GE, #LE, cut)
     // and the vector's M slots (a one-wave round: only its 512 segment slots)
@@ -112,7 +120,19 @@ constexpr uint32_t kTrHead = 8;
 #else
 [[maybe_unused]] constexpr bool kStampsSmall = false;
 #endif
-#if defined(SVO_STAMPS)
+#if defined(SVO_STAMPS) && defined(SVO_STAMPS_WAVES)
+#define VSTAMP(i) \
+    do { \
+        if (kStampOn && dg && lane == 0) { \
+            const uint64_t t_ = clock64(); \
+            if (!kStampsSmall || small_round) { \
+                dg->phw[wave][i] += (uint32_t)(t_ - tstamp); \
+                if (tid == 0) dg->ph[i] += t_ - tstamp; \
+            } \
+            tstamp = t_; \
+        } \
+    } while (0)
+#elif defined(SVO_STAMPS)
 #define VSTAMP(i) \
     do { \
         if (kStampOn && dg && tid == 0) { \
@@ -722,25 +742,48 @@ struct VSel {
         counts(C);
         VSTAMP(8);
         const uint32_t totL = C.totL, totG = C.totG;
-        // the crossing: the last step whose start has G < Lc, i.e. G + L < totL (the segment's first step always)
-        uint32_t pke;
-        const uint32_t es = find_step(C, 2, totL, pke);
-        const uint64_t mge = rec_mask(es, 0), mle = rec_mask(es, 1);
-        const uint32_t ks = uni(wave_crossing_ks(pke & 0xFFFFu, totL - (pke >> 16), mge, mle));
-        VSTAMP(9);
-        // L_{Ks+1} (GE rank Ks + 1), R_{Ks} (LE rank totL - Ks + 1 from the left), L_{Ks}: all three sit next to the
-        // crossing split, so they are looked for in the crossing step first
-        const uint32_t ra = ks + 1u, rb = totL - ks + 1u, rc = ks;
-        const uint32_t G0 = pke & 0xFFFFu, L0 = pke >> 16, cg = popc(mge), cl = popc(mle);
-        const uint32_t ebase = es * 64u;
-        const uint32_t lk1 = ra > totG ? kNone
-                             : (ra > G0 && ra <= G0 + cg) ? ebase + uni(wave_select_bit(mge, ra - G0 - 1u)) : uni(locate(C, 0, ra));
-        const uint32_t rk = ks == 0 ? kNone
-                            : (rb > L0 && rb <= L0 + cl) ? ebase + uni(wave_select_bit(mle, rb - L0 - 1u)) : uni(locate(C, 1, rb));
-        const uint32_t lk = ks == 0 ? kNone
-                            : (rc > G0 && rc <= G0 + cg) ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : uni(locate(C, 0, rc));
+        uint32_t ks, lk1, rk, lk;
+        auto search = [&]() __attribute__((always_inline)) {
+            // the crossing: the last step whose start has G < Lc, i.e. G + L < totL (the segment's first step always)
+            uint32_t pke;
+            const uint32_t es = find_step(C, 2, totL, pke);
+            const uint64_t mge = rec_mask(es, 0), mle = rec_mask(es, 1);
+            ks = uni(wave_crossing_ks(pke & 0xFFFFu, totL - (pke >> 16), mge, mle));
+            VSTAMP(9);
+            // L_{Ks+1} (GE rank Ks + 1), R_{Ks} (LE rank totL - Ks + 1 from the left), L_{Ks}: all three sit next to
+            // the crossing split, so they are looked for in the crossing step first
+            const uint32_t ra = ks + 1u, rb = totL - ks + 1u, rc = ks;
+            const uint32_t G0 = pke & 0xFFFFu, L0 = pke >> 16, cg = popc(mge), cl = popc(mle);
+            const uint32_t ebase = es * 64u;
+            lk1 = ra > totG ? kNone
+                  : (ra > G0 && ra <= G0 + cg) ? ebase + uni(wave_select_bit(mge, ra - G0 - 1u)) : uni(locate(C, 0, ra));
+            rk = ks == 0 ? kNone
+                 : (rb > L0 && rb <= L0 + cl) ? ebase + uni(wave_select_bit(mle, rb - L0 - 1u)) : uni(locate(C, 1, rb));
+            lk = ks == 0 ? kNone
+                 : (rc > G0 && rc <= G0 + cg) ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : uni(locate(C, 0, rc));
+            VSTAMP(10);
+        };
+#if defined(SVO_K2V_ONECHAIN)
+        // the scalar search chain once, on wave 0 (the oldest wave, first in issue); the others wait at a barrier
+        // instead of running seven more copies of it beside their SIMD partners, then read the four results
+        if (wave == 0) {
+            search();
+            if (lane == 0) {
+                sh.srch[0] = ks;
+                sh.srch[1] = lk1;
+                sh.srch[2] = rk;
+                sh.srch[3] = lk;
+            }
+        }
+        __syncthreads();
+        ks = uni(sh.srch[0]);
+        lk1 = uni(sh.srch[1]);
+        rk = uni(sh.srch[2]);
+        lk = uni(sh.srch[3]);
+#else
+        search();
+#endif
         const uint32_t cut = lk1 < rk ? lk1 : rk;
-        VSTAMP(10);
         const bool right = cut <= nth;  // the side introselect continues with
         const uint32_t nf = right ? cut : f, nl = right ? l : cut;
         // vec[nth - 1] after this round (never touched again): only L_{Ks} can sit at cut - 1
@@ -795,7 +838,7 @@ struct VSel {
         if (nch > 1) __syncthreads();  // (records read above until here)
         VSTAMP(6);
         if (dg && tid == 0) dg->nchunk[P] += nch > 1 ? 1u : 0u;
-#if defined(SVO_STAMPS)
+#if defined(SVO_STAMPS) && !defined(SVO_STAMPS_WAVES)
         if (kStampOn && dg && tid == 0 && dg->nlog < 64) {
             dg->log[dg->nlog][0] = S0;
             dg->log[dg->nlog][1] = (uint32_t)(clock64() - tround);
@@ -1189,7 +1232,11 @@ __global__ void __launch_bounds__(kVT, 1) debug_robust_scale_v_kernel(const doub
             out[6 + 5 * P] = (double)dg.nchunk[P];
         }
         for (int i = 0; i < 12; ++i) out[12 + i] = (double)dg.ph[i];
+#if defined(SVO_STAMPS_WAVES)
+        for (int i = 0; i < 128; ++i) out[24 + i] = i < 12 * kVW ? (double)dg.phw[i / 12][i % 12] : -1.0;
+#else
         for (int i = 0; i < 128; ++i) out[24 + i] = i / 2 < (int)dg.nlog ? (double)dg.log[i / 2][i % 2] : -1.0;
+#endif
     }
 }
 

@@ -222,35 +222,43 @@ __device__ __forceinline__ uint32_t load4(const uint8_t* plane, int W, int row, 
 }
 
 // one output row run of a wave: lanes 1..own hold K bytes each (little-endian in v) for columns
-// col0 + K (l - 1) + i; columns in [col0, ncol) are written to dst_row (the plane row's column 0)
+// col0 + K (l - 1) + i; columns in [col0, ncol) go to dst_row (the plane row's column 0).  stage_run writes the
+// lane's bytes into the wave's LDS buffer at the run's address alignment; flush_run (after the stages of every run
+// of the row: one LDS round trip for all of them) stores the buffer as aligned dwords, the run's partial end dwords
+// byte by byte.
+struct Run {
+    uintptr_t A;  // address of the run's first byte
+    int n;        // bytes from the aligned dword below A to the run's end (0: empty run)
+};
 template <int K>
-__device__ __forceinline__ void store_run(uint8_t* dst_row, int col0, int ncol, int own, uint32_t v, uint8_t* lbuf,
-                                          int lane) {
+__device__ __forceinline__ Run stage_run(uint8_t* dst_row, int col0, int ncol, int own, uint32_t v, uint8_t* lbuf,
+                                         int lane) {
     const int ch = min(col0 + K * own, ncol);
-    if (ch <= col0) return;  // (wave-uniform)
-    const uintptr_t A = reinterpret_cast<uintptr_t>(dst_row + col0);
-    const int sh = (int)(A & 3u);
-    const int n = sh + (ch - col0);
+    Run r{reinterpret_cast<uintptr_t>(dst_row + col0), 0};
+    if (ch <= col0) return r;  // (wave-uniform)
+    const int sh = (int)(r.A & 3u);
+    r.n = sh + (ch - col0);
     if (lane >= 1 && lane <= own) {
         const int c = K * (lane - 1);
 #pragma unroll
         for (int i = 0; i < K; ++i)
             if (col0 + c + i < ch) lbuf[sh + c + i] = (uint8_t)(v >> (8 * i));
     }
-    asm volatile("" ::: "memory");  // (the dword reads below take other lanes' bytes: in order within the wave)
+    return r;
+}
+__device__ __forceinline__ void flush_run(const Run& r, const uint8_t* lbuf, int lane) {
     const int lo = 4 * lane;
-    if (lo < n) {
-        const uint32_t w = reinterpret_cast<const uint32_t*>(lbuf)[lane];
-        uint8_t* g = reinterpret_cast<uint8_t*>(A & ~(uintptr_t)3) + lo;
-        if (lo >= sh && lo + 4 <= n) {
-            *reinterpret_cast<uint32_t*>(g) = w;
-        } else {
+    if (lo >= r.n) return;
+    const int sh = (int)(r.A & 3u);
+    const uint32_t w = reinterpret_cast<const uint32_t*>(lbuf)[lane];
+    uint8_t* g = reinterpret_cast<uint8_t*>(r.A & ~(uintptr_t)3) + lo;
+    if (lo >= sh && lo + 4 <= r.n) {
+        *reinterpret_cast<uint32_t*>(g) = w;
+    } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (lo + i >= sh && lo + i < n) g[i] = (uint8_t)(w >> (8 * i));
-        }
+        for (int i = 0; i < 4; ++i)
+            if (lo + i >= sh && lo + i < r.n) g[i] = (uint8_t)(w >> (8 * i));
     }
-    asm volatile("" ::: "memory");  // (the next run rewrites the buffer)
 }
 
 typedef uint16_t u16x2v __attribute__((ext_vector_type(2)));
@@ -291,12 +299,12 @@ __device__ __forceinline__ uint32_t hpass(uint32_t ev, uint32_t od, int c0, int 
 __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
                                                                  int W, int H, int64_t off1, int W1, int H1, int own,
                                                                  int nstrip, int nband, int first) {
-    __shared__ __attribute__((aligned(16))) uint8_t lbuf_all[kL01Waves][256];
+    __shared__ __attribute__((aligned(16))) uint8_t lbuf_all[kL01Waves][4][256];  // per wave: one buffer per run
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int gw = blockIdx.x * kL01Waves + wv;
     if (gw >= nstrip * nband) return;  // (wave-uniform)
     const int strip = gw % nstrip, band = gw / nstrip;
-    uint8_t* const lbuf = lbuf_all[wv];
+    uint8_t(*const lbuf)[256] = lbuf_all[wv];
     const int frame = first + blockIdx.y;
     uint8_t* const ibase = stacks + frame * frame_stride;
     uint8_t* const gbase = ibase + grad_off;
@@ -317,31 +325,43 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01_kernel(uint8_t* stacks
         const int py = row_of(y);
         return (py == 0 || py == H - 1) ? 0u : (g & colmask);
     };
-    // window: R[k] = base row (logical) 2r - 3 + k, G[i] = gradient row 2r - 2 + i
-    uint32_t R[7], G[5];
+    // window: R[k] = base row (logical) 2r - 3 + k, G[i] = gradient row 2r - 2 + i; P: the base rows of the next
+    // two iterations, in flight
+    uint32_t R[7], G[5], P[4];
 #pragma unroll
     for (int k = 0; k < 7; ++k) R[k] = ld(2 * r0 - 3 + k);
 #pragma unroll
+    for (int k = 0; k < 4; ++k) P[k] = ld(2 * r0 + 4 + k);
+#pragma unroll
     for (int i = 0; i < 5; ++i) G[i] = grad(R[i], R[i + 1], R[i + 2], 2 * r0 - 2 + i);
     for (int r = r0; r < r1; ++r) {
-        // the next two base rows go out first (in flight during this row's work)
-        const uint32_t n5 = ld(2 * r + 4), n6 = ld(2 * r + 5);
-        // level-0 gradient rows 2r, 2r + 1 (this band's own source rows)
-        store_run<4>(gbase + (int64_t)(2 * r) * W, col0, W, own, G[2], lbuf, lane);
-        if (2 * r + 1 < H) store_run<4>(gbase + (int64_t)(2 * r + 1) * W, col0, W, own, G[3], lbuf, lane);
         // level 1 of both stacks
         uint32_t ev, od;
         vsum5(R[1], R[2], R[3], R[4], R[5], ev, od);
         const uint32_t oi = hpass(ev, od, c0, W, edge);
         vsum5(G[0], G[1], G[2], G[3], G[4], ev, od);
         const uint32_t og = hpass(ev, od, c0, W, edge);
-        store_run<2>(ibase + off1 + (int64_t)r * W1, col0 / 2, W1, own, oi, lbuf, lane);
-        store_run<2>(gbase + off1 + (int64_t)r * W1, col0 / 2, W1, own, og, lbuf, lane);
+        // the row's four runs: level-0 gradient rows 2r, 2r + 1 (this band's own source rows), level-1 rows
+        const Run q0 = stage_run<4>(gbase + (int64_t)(2 * r) * W, col0, W, own, G[2], lbuf[0], lane);
+        const Run q1 = 2 * r + 1 < H ? stage_run<4>(gbase + (int64_t)(2 * r + 1) * W, col0, W, own, G[3], lbuf[1], lane)
+                                     : Run{0, 0};
+        const Run q2 = stage_run<2>(ibase + off1 + (int64_t)r * W1, col0 / 2, W1, own, oi, lbuf[2], lane);
+        const Run q3 = stage_run<2>(gbase + off1 + (int64_t)r * W1, col0 / 2, W1, own, og, lbuf[3], lane);
+        asm volatile("" ::: "memory");  // (the dword reads take other lanes' bytes: LDS keeps a wave's order)
+        flush_run(q0, lbuf[0], lane);
+        flush_run(q1, lbuf[1], lane);
+        flush_run(q2, lbuf[2], lane);
+        flush_run(q3, lbuf[3], lane);
+        asm volatile("" ::: "memory");  // (the next row rewrites the buffers)
         // advance the window by two base rows
 #pragma unroll
         for (int k = 0; k < 5; ++k) R[k] = R[k + 2];
-        R[5] = n5;
-        R[6] = n6;
+        R[5] = P[0];
+        R[6] = P[1];
+        P[0] = P[2];
+        P[1] = P[3];
+        P[2] = ld(2 * r + 8);
+        P[3] = ld(2 * r + 9);
 #pragma unroll
         for (int i = 0; i < 3; ++i) G[i] = G[i + 2];
         G[3] = grad(R[3], R[4], R[5], 2 * r + 3);
@@ -349,10 +369,185 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01_kernel(uint8_t* stacks
     }
 }
 
-bool use_l01() {
-    static const bool old = getenv("SVO_PYR") && atoi(getenv("SVO_PYR")) == 0;  // (measurement knob, read once)
-    return !old;
+// ---------------------------------------------------------------------------------------------------------------
+// pyr_l01v2_kernel: the same pass with every row kept unpacked as well (u16 pairs of columns (0, 2) and (1, 3)), the
+// gradient, the vertical sums and the horizontal pass all on packed u16 pairs (the horizontal [1 4 6 4 1] sum of
+// level-1 sums stays below 2^16), the row addresses on scalars (the rows' alignment is uniform: every lane's c0 is
+// a multiple of 4), and the outputs stored straight from the lanes: a dword per lane per gradient row and a 16-bit
+// pair per lane per level-1 row, at their (unaligned) addresses; the lanes at the right edge store byte by byte.
+struct Px4 {
+    uint32_t p, e, o;  // four pixels; columns (0, 2) and (1, 3) as u16 pairs
+};
+__device__ __forceinline__ uint32_t pe(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C020C00u); }  // b0, b2
+__device__ __forceinline__ uint32_t po(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C030C01u); }  // b1, b3
+__device__ __forceinline__ uint32_t pk_absdiff(uint32_t a, uint32_t b) {
+    return as_u32(__builtin_elementwise_max(as_u16x2(a), as_u16x2(b)) - __builtin_elementwise_min(as_u16x2(a), as_u16x2(b)));
 }
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return as_u32(as_u16x2(a) + as_u16x2(b)); }
+// [1 4 6 4 1] over five u16 pairs (every sum of this pyramid stays below 2^16)
+__device__ __forceinline__ uint32_t pk_tap5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
+    const u16x2v s = (as_u16x2(a) + as_u16x2(e)) + ((as_u16x2(b) + as_u16x2(d)) << (u16x2v){2, 2}) +
+                     as_u16x2(c) * (u16x2v){6, 6};
+    return as_u32(s);
+}
+
+// one strip x band of pyr_l01v2_kernel; kLE / kRE: the strip holds column 0 / column W - 1 (reflected taps, the
+// partial last lanes), so the interior strips carry none of that code
+template <bool kLE, bool kRE>
+__device__ __forceinline__ void l01v2_strip(uint8_t* ibase, uint8_t* gbase, int W, int H, int64_t off1, int W1, int own,
+                                            int col0, int r0, int r1, int lane) {
+    const int c0 = col0 + 4 * (lane - 1);
+    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;  // the lane's load column (never used when clamped)
+    const bool owner = lane >= 1 && lane <= own;
+    // the gradient's border columns (Simd leaves them 0) as u16-pair masks
+    uint32_t me = 0xFFFFFFFFu, mo = 0xFFFFFFFFu;
+    if (kLE && c0 == 0) me &= 0xFFFF0000u;
+    if (kRE) {
+        if (c0 == W - 1) me &= 0xFFFF0000u;
+        if (c0 + 2 == W - 1) me &= 0x0000FFFFu;
+        if (c0 + 1 == W - 1) mo &= 0xFFFF0000u;
+        if (c0 + 3 == W - 1) mo &= 0x0000FFFFu;
+    }
+    const uint8_t* const lbase = ibase + cl;
+    // (uniform) the aligned offset of row refl101(y) and its byte shift: every lane's c0 is 0 mod 4
+    auto rowoff = [&](int y, uint32_t& sh) -> int64_t {
+        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
+        sh = (uint32_t)(ro & 3);
+        return ro & ~(int64_t)3;
+    };
+    auto raw = [&](int y) -> uint32_t {
+        uint32_t sh;
+        return *reinterpret_cast<const uint32_t*>(lbase + rowoff(y, sh));
+    };
+    auto cook = [&](uint32_t lo, int y) -> Px4 {
+        uint32_t sh;
+        (void)rowoff(y, sh);
+        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, sh);
+        return Px4{v, pe(v), po(v)};
+    };
+    auto grad = [&](const Px4& up, const Px4& mid, const Px4& dn, int y, uint32_t& ge, uint32_t& go) {
+        const uint32_t L = from_left(mid.p), R = from_right(mid.p);
+        const uint32_t l = __builtin_amdgcn_alignbyte(mid.p, L, 3), r = __builtin_amdgcn_alignbyte(R, mid.p, 1);
+        const u16x2v lim = {255, 255};
+        ge = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(pe(l), pe(r)), pk_absdiff(up.e, dn.e))), lim));
+        go = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(po(l), po(r)), pk_absdiff(up.o, dn.o))), lim));
+        const int py = __builtin_amdgcn_readfirstlane(refl101(y, H));
+        if (py == 0 || py == H - 1) {  // (uniform)
+            ge = 0u;
+            go = 0u;
+        }
+        if (kLE || kRE) {
+            ge &= me;
+            go &= mo;
+        }
+    };
+    // the two level-1 pixels of the lane from the vertical sums ev (columns 0, 2), od (1, 3): packed pairs
+    // A = (c-2, c0), B = (c-1, c1), C = (c0, c2), D = (c1, c3), E = (c2, c4) -> (x0, x1) = A + 4B + 6C + 4D + E
+    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
+        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
+        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
+        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
+        if (kLE && c0 == 0) {  // columns -2, -1 -> 2, 1 (BORDER_REFLECT_101)
+            A = (A & 0xFFFF0000u) | (C >> 16);
+            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
+        }
+        if (kRE) {  // columns >= W -> 2W - 2 - c, for the outputs this lane stores
+            const int d = W - 1 - c0;
+            if (d == 0) {  // x0 only: c1 <- c-1, c2 <- c-2
+                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
+                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
+            } else if (d == 1) {  // x0 only: c2 <- c0
+                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
+            } else if (d == 2) {  // x1: c3 <- c1, c4 <- c0
+                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
+                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
+            } else if (d == 3) {  // x1: c4 <- c2
+                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
+            }
+        }
+        const u16x2v t = as_u16x2(pk_tap5(A, B, C, D, E)) + (u16x2v){128, 128};
+        const uint32_t q = as_u32(t >> (u16x2v){8, 8});
+        return __builtin_amdgcn_perm(0u, q, 0x0C0C0200u);  // x0 | x1 << 8
+    };
+    // stores: a dword (gradient row) / a 16-bit pair (level-1 row) per owner lane at its own address; the lanes
+    // holding the row's last column write their part byte by byte
+    const bool full_g = owner && (!kRE || c0 + 3 < W), part_g = kRE && owner && c0 < W && c0 + 3 >= W;
+    const int x = c0 >> 1;
+    const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
+    auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
+        const uint32_t v = ge | (go << 8);
+        uint8_t* const d = gbase + (int64_t)__builtin_amdgcn_readfirstlane(y * W) + c0;
+        if (full_g) *reinterpret_cast<uint32_t*>(d) = v;
+        if (kRE && part_g)
+            for (int i = 0; i < 4; ++i)
+                if (c0 + i < W) d[i] = (uint8_t)(v >> (8 * i));
+    };
+    auto store_l1 = [&](uint8_t* plane, int r, uint32_t v) {
+        uint8_t* const d = plane + off1 + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
+        if (full_1) *reinterpret_cast<uint16_t*>(d) = (uint16_t)v;
+        if (kRE && part_1) d[0] = (uint8_t)v;
+    };
+    Px4 R[7];
+    uint32_t GE[5], GO[5];
+    uint32_t P[4];  // raw aligned dwords of the next two iterations' rows (in flight)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) R[k] = cook(raw(2 * r0 - 3 + k), 2 * r0 - 3 + k);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) grad(R[i], R[i + 1], R[i + 2], 2 * r0 - 2 + i, GE[i], GO[i]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) P[k] = raw(2 * r0 + 4 + k);
+#pragma unroll 2
+    for (int r = r0; r < r1; ++r) {
+        store_grad(2 * r, GE[2], GO[2]);
+        if (2 * r + 1 < H) store_grad(2 * r + 1, GE[3], GO[3]);
+        const uint32_t ei = pk_tap5(R[1].e, R[2].e, R[3].e, R[4].e, R[5].e);
+        const uint32_t oi = pk_tap5(R[1].o, R[2].o, R[3].o, R[4].o, R[5].o);
+        store_l1(ibase, r, hpass2(ei, oi));
+        const uint32_t eg = pk_tap5(GE[0], GE[1], GE[2], GE[3], GE[4]);
+        const uint32_t og = pk_tap5(GO[0], GO[1], GO[2], GO[3], GO[4]);
+        store_l1(gbase, r, hpass2(eg, og));
+#pragma unroll
+        for (int k = 0; k < 5; ++k) R[k] = R[k + 2];
+        R[5] = cook(P[0], 2 * r + 4);
+        R[6] = cook(P[1], 2 * r + 5);
+        P[0] = P[2];
+        P[1] = P[3];
+        P[2] = raw(2 * r + 8);
+        P[3] = raw(2 * r + 9);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            GE[i] = GE[i + 2];
+            GO[i] = GO[i + 2];
+        }
+        grad(R[3], R[4], R[5], 2 * r + 3, GE[3], GO[3]);
+        grad(R[4], R[5], R[6], 2 * r + 4, GE[4], GO[4]);
+    }
+}
+
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v2_kernel(uint8_t* stacks, int64_t frame_stride,
+                                                                   int64_t grad_off, int W, int H, int64_t off1, int W1,
+                                                                   int H1, int own, int nstrip, int nband, int first) {
+    // (the wave index through readfirstlane: everything derived from it is uniform and lives in SGPRs)
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = blockIdx.x * kL01Waves + wv;
+    if (gw >= nstrip * nband) return;  // (wave-uniform)
+    const int strip = gw % nstrip, band = gw / nstrip;
+    uint8_t* const ibase = stacks + (first + (int64_t)blockIdx.y) * frame_stride;
+    uint8_t* const gbase = ibase + grad_off;
+    const int col0 = 4 * own * strip;
+    const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
+    const bool le = strip == 0, re = col0 + 4 * own >= W;
+    if (le && re) l01v2_strip<true, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else if (le) l01v2_strip<true, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else if (re) l01v2_strip<false, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else l01v2_strip<false, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+}
+
+int pyr_mode() {  // SVO_PYR: 0 the round-4 kernels, 1 pyr_l01_kernel, 2 (default) pyr_l01v2_kernel (measurement knob)
+    static const int m = getenv("SVO_PYR") ? atoi(getenv("SVO_PYR")) : 2;
+    return m;
+}
+
 
 }  // namespace
 
@@ -363,15 +558,15 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
     const int64_t stride = (grad_off + g.frame_bytes + 255) / 256 * 256;
     const int64_t npx = (int64_t)g.w[0] * g.h[0];
     int l = 1;
-    if (g.levels >= 2 && use_l01()) {
+    if (g.levels >= 2 && pyr_mode() != 0) {
         // strips of `own` lanes x 4 columns (<= 62 lanes: lanes 0 and 63 are halo), as few strips as the width needs
         const int nstrip = (g.w[0] + 4 * 62 - 1) / (4 * 62);
         const int own = (g.w[0] + 4 * nstrip - 1) / (4 * nstrip);
         const int nband = (g.h[1] + kL01Band - 1) / kL01Band;
         const int waves = nstrip * nband;
-        hipLaunchKernelGGL(pyr_l01_kernel, dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count),
-                           dim3(64 * kL01Waves), 0, s, stacks, stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1],
-                           own, nstrip, nband, first);
+        hipLaunchKernelGGL(pyr_mode() == 1 ? pyr_l01_kernel : pyr_l01v2_kernel,
+                           dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count), dim3(64 * kL01Waves), 0, s, stacks,
+                           stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1], own, nstrip, nband, first);
         l = 2;
     } else {
         hipLaunchKernelGGL(abs_grad_kernel, dim3((unsigned)((npx + kGradRun - 1) / kGradRun), count), dim3(kGradThreads), 0,

@@ -45,8 +45,15 @@ if impl == svo_amd.SCALE_K2V:
     names = ("load", "classify", "barrier1", "publish+ranks", "sources", "barrier2", "targets", "exits", "scan",
              "crossing", "searches")
     print("K2V cycles per phase (thread 0, both passes): " + ", ".join(f"{a} {x:.0f}" for a, x in zip(names, out[12:23])))
-    log = out[24:152].reshape(-1, 2)
-    print("K2V block rounds (S, cycles; stamps build):", [tuple(int(x) for x in r) for r in log if r[0] >= 0])
+    if os.environ.get("SVO_PROBE_WAVES"):  # (make stamps STAMPS_WAVES=1: every wave's cycles per phase)
+        pw = out[24:24 + 96].reshape(8, 12)
+        print("K2V cycles per phase and wave (both passes; rows: waves 0-7):")
+        print("      " + " ".join(f"{a[:9]:>9}" for a in names))
+        for w in range(8):
+            print(f"  w{w}  " + " ".join(f"{x:9.0f}" for x in pw[w, :11]))
+    else:
+        log = out[24:152].reshape(-1, 2)
+        print("K2V block rounds (S, cycles; stamps build):", [tuple(int(x) for x in r) for r in log if r[0] >= 0])
     sys.exit(0 if match else 3)
 for p in range(2):
     cyc, nb, nl, hp = out[2 + 4 * p: 6 + 4 * p]
