@@ -85,7 +85,7 @@ struct VShared {
     double pub[6];                    // pre-values published by their owners (candidates 0-3, record 4)
     uint32_t pubk[4];                 // the candidates' target ranks (0: not a target), by their owners
     double bcd;                       // broadcast of the median between the passes
-    uint32_t srch[4];                 // (SVO_K2V_ONECHAIN) Ks, L_{Ks+1}, R_{Ks}, L_{Ks} from wave 0
+    uint32_t srch[4];                 // Ks, L_{Ks+1}, R_{Ks}, L_{Ks} from wave 0
     double lrow[L::kRows - L::kRegRows][kVT];  // the LDS rows of the vector (the rest is in registers)
     uint32_t tmp[2 * kVW];            // per-wave counts of the prologue
 };
@@ -763,9 +763,11 @@ struct VSel {
                  : (rc > G0 && rc <= G0 + cg) ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : uni(locate(C, 0, rc));
             VSTAMP(10);
         };
-#if defined(SVO_K2V_ONECHAIN)
+#if !defined(SVO_K2V_ALLCHAINS)
         // the scalar search chain once, on wave 0 (the oldest wave, first in issue); the others wait at a barrier
         // instead of running seven more copies of it beside their SIMD partners, then read the four results
+        // (round 5, same box A/B: 165.6k -> 166.9k pairs/s alone, 168.7k -> 170.2k on top of the ILP quads;
+        // -DSVO_K2V_ALLCHAINS builds round 4's every-wave form)
         if (wave == 0) {
             search();
             if (lane == 0) {

@@ -199,11 +199,12 @@ __global__ void __launch_bounds__(kGradThreads) abs_grad_kernel(uint8_t* stacks,
 constexpr int kL01Waves = 4;                  // independent waves per workgroup (strip x band each)
 constexpr int kL01Band = 32;                  // level-1 rows per band
 
+// (bound_ctrl: the lane without a source reads 0; no "old" operand to materialize)
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {   // lane i <- lane i - 1 (wave_shr:1)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t from_right(uint32_t v) {  // lane i <- lane i + 1 (wave_shl:1)
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xF, 0xF, true);
 }
 __device__ __forceinline__ int refl101(int i, int n) {  // one reflection (valid taps never need two) + clamp
     i = i < 0 ? -i : i;
@@ -543,8 +544,293 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v2_kernel(uint8_t* stac
     else l01v2_strip<false, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
 }
 
-int pyr_mode() {  // SVO_PYR: 0 the round-4 kernels, 1 pyr_l01_kernel, 2 (default) pyr_l01v2_kernel (measurement knob)
-    static const int m = getenv("SVO_PYR") ? atoi(getenv("SVO_PYR")) : 2;
+// ---------------------------------------------------------------------------------------------------------------
+// pyr_l01v3_kernel: pyr_l01v2's arithmetic with the vertical [1 4 6 4 1] pass as running sums instead of a window of
+// rows: source row 2m + 1 adds 4x to level-1 rows m and m + 1, row 2m adds 1x / 6x / 1x to rows m - 1, m, m + 1, so
+// a lane carries two partial sums per stack and the four base rows the gradient needs, and every role alternates
+// between two register sets from one step to the next: the loop, unrolled by two, moves no register.
+struct Acc {
+    uint32_t ie, io, ge, go;  // intensity / gradient partial sums, columns (0, 2) and (1, 3)
+};
+__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c on u16 pairs
+    return as_u32(as_u16x2(a) * (u16x2v){(uint16_t)k, (uint16_t)k} + as_u16x2(c));
+}
+
+template <bool kLE, bool kRE>
+__device__ __forceinline__ void l01v3_strip(uint8_t* ibase, uint8_t* gbase, int W, int H, int64_t off1, int W1, int own,
+                                            int col0, int r0, int r1, int lane) {
+    const int c0 = col0 + 4 * (lane - 1);
+    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;  // the lane's load column (never used when clamped)
+    const bool owner = lane >= 1 && lane <= own;
+    uint32_t me = 0xFFFFFFFFu, mo = 0xFFFFFFFFu;  // the gradient's border columns as u16-pair masks
+    if (kLE && c0 == 0) me &= 0xFFFF0000u;
+    if (kRE) {
+        if (c0 == W - 1) me &= 0xFFFF0000u;
+        if (c0 + 2 == W - 1) me &= 0x0000FFFFu;
+        if (c0 + 1 == W - 1) mo &= 0xFFFF0000u;
+        if (c0 + 3 == W - 1) mo &= 0x0000FFFFu;
+    }
+    const uint8_t* const lbase = ibase + cl;
+    auto rowoff = [&](int y, uint32_t& sh) -> int64_t {
+        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
+        sh = (uint32_t)(ro & 3);
+        return ro & ~(int64_t)3;
+    };
+    auto raw = [&](int y) -> uint32_t {
+        uint32_t sh;
+        return *reinterpret_cast<const uint32_t*>(lbase + rowoff(y, sh));
+    };
+    auto cook = [&](uint32_t lo, int y) -> Px4 {
+        uint32_t sh;
+        (void)rowoff(y, sh);
+        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, sh);
+        return Px4{v, pe(v), po(v)};
+    };
+    auto grad = [&](const Px4& up, const Px4& mid, const Px4& dn, int y, uint32_t& ge, uint32_t& go) {
+        const uint32_t L = from_left(mid.p), R = from_right(mid.p);
+        const uint32_t l = __builtin_amdgcn_alignbyte(mid.p, L, 3), r = __builtin_amdgcn_alignbyte(R, mid.p, 1);
+        const u16x2v lim = {255, 255};
+        ge = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(pe(l), pe(r)), pk_absdiff(up.e, dn.e))), lim));
+        go = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(po(l), po(r)), pk_absdiff(up.o, dn.o))), lim));
+        const int py = __builtin_amdgcn_readfirstlane(refl101(y, H));
+        if (py == 0 || py == H - 1) {  // (uniform)
+            ge = 0u;
+            go = 0u;
+        }
+        if (kLE || kRE) {
+            ge &= me;
+            go &= mo;
+        }
+    };
+    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
+        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
+        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
+        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
+        if (kLE && c0 == 0) {  // columns -2, -1 -> 2, 1 (BORDER_REFLECT_101)
+            A = (A & 0xFFFF0000u) | (C >> 16);
+            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
+        }
+        if (kRE) {  // columns >= W -> 2W - 2 - c, for the outputs this lane stores
+            const int d = W - 1 - c0;
+            if (d == 0) {
+                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
+                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
+            } else if (d == 1) {
+                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
+            } else if (d == 2) {
+                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
+                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
+            } else if (d == 3) {
+                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
+            }
+        }
+        const u16x2v t = as_u16x2(pk_tap5(A, B, C, D, E)) + (u16x2v){128, 128};
+        const uint32_t q = as_u32(t >> (u16x2v){8, 8});
+        return __builtin_amdgcn_perm(0u, q, 0x0C0C0200u);  // x0 | x1 << 8
+    };
+    const bool full_g = owner && (!kRE || c0 + 3 < W), part_g = kRE && owner && c0 < W && c0 + 3 >= W;
+    const int x = c0 >> 1;
+    const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
+    const int ylim = min(2 * r1, H);  // this band's own base rows: [2 r0, ylim)
+    auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
+        if (y >= ylim) return;  // (uniform)
+        const uint32_t v = ge | (go << 8);
+        uint8_t* const d = gbase + (int64_t)__builtin_amdgcn_readfirstlane(y * W) + c0;
+        if (full_g) *reinterpret_cast<uint32_t*>(d) = v;
+        if (kRE && part_g)
+            for (int i = 0; i < 4; ++i)
+                if (c0 + i < W) d[i] = (uint8_t)(v >> (8 * i));
+    };
+    auto store_l1 = [&](uint8_t* plane, int r, uint32_t v) {
+        uint8_t* const d = plane + off1 + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
+        if (full_1) *reinterpret_cast<uint16_t*>(d) = (uint16_t)v;
+        if (kRE && part_1) d[0] = (uint8_t)v;
+    };
+    // one level-1 row r: holds I(2r), I(2r + 1) in I0, I1, takes the raw rows 2r + 2, 2r + 3 from Pa, Pb (reloads
+    // them with 2r + 6, 2r + 7), leaves I(2r + 2), I(2r + 3) in I2, I3; X: the sums of row r (completed and stored
+    // here, then restarted as row r + 2's), Y: row r + 1's
+    auto step = [&](int r, const Px4& I0, const Px4& I1, Px4& I2, Px4& I3, uint32_t& Pa, uint32_t& Pb, Acc& X, Acc& Y) {
+        I2 = cook(Pa, 2 * r + 2);
+        I3 = cook(Pb, 2 * r + 3);
+        Pa = raw(2 * r + 6);
+        Pb = raw(2 * r + 7);
+        uint32_t g1e, g1o, g2e, g2o;
+        grad(I0, I1, I2, 2 * r + 1, g1e, g1o);
+        grad(I1, I2, I3, 2 * r + 2, g2e, g2o);
+        store_grad(2 * r + 1, g1e, g1o);
+        store_grad(2 * r + 2, g2e, g2o);
+        // row 2r + 1: 4x into rows r and r + 1; row 2r + 2: 1x into r (complete), 6x into r + 1, 1x starts r + 2
+        X.ie = pk_add(pk_mad(I1.e, 4, X.ie), I2.e);
+        X.io = pk_add(pk_mad(I1.o, 4, X.io), I2.o);
+        X.ge = pk_add(pk_mad(g1e, 4, X.ge), g2e);
+        X.go = pk_add(pk_mad(g1o, 4, X.go), g2o);
+        Y.ie = pk_mad(I2.e, 6, pk_mad(I1.e, 4, Y.ie));
+        Y.io = pk_mad(I2.o, 6, pk_mad(I1.o, 4, Y.io));
+        Y.ge = pk_mad(g2e, 6, pk_mad(g1e, 4, Y.ge));
+        Y.go = pk_mad(g2o, 6, pk_mad(g1o, 4, Y.go));
+        store_l1(ibase, r, hpass2(X.ie, X.io));
+        store_l1(gbase, r, hpass2(X.ge, X.go));
+        X = Acc{I2.e, I2.o, g2e, g2o};
+    };
+    // the state at r0: I(2r0 - 3 .. 2r0 + 1), gradients 2r0 - 2 .. 2r0, row r0's sums over 2r0 - 2 .. 2r0, row
+    // r0 + 1's over 2r0
+    Px4 Ia, Ib, Ic, Id;
+    Acc X, Y;
+    {
+        const Px4 Jm3 = cook(raw(2 * r0 - 3), 2 * r0 - 3), Jm2 = cook(raw(2 * r0 - 2), 2 * r0 - 2);
+        const Px4 Jm1 = cook(raw(2 * r0 - 1), 2 * r0 - 1);
+        Ia = cook(raw(2 * r0), 2 * r0);
+        Ib = cook(raw(2 * r0 + 1), 2 * r0 + 1);
+        uint32_t hm2e, hm2o, hm1e, hm1o, h0e, h0o;
+        grad(Jm3, Jm2, Jm1, 2 * r0 - 2, hm2e, hm2o);
+        grad(Jm2, Jm1, Ia, 2 * r0 - 1, hm1e, hm1o);
+        grad(Jm1, Ia, Ib, 2 * r0, h0e, h0o);
+        store_grad(2 * r0, h0e, h0o);
+        X.ie = pk_mad(Ia.e, 6, pk_mad(Jm1.e, 4, Jm2.e));
+        X.io = pk_mad(Ia.o, 6, pk_mad(Jm1.o, 4, Jm2.o));
+        X.ge = pk_mad(h0e, 6, pk_mad(hm1e, 4, hm2e));
+        X.go = pk_mad(h0o, 6, pk_mad(hm1o, 4, hm2o));
+        Y = Acc{Ia.e, Ia.o, h0e, h0o};
+    }
+    uint32_t P0 = raw(2 * r0 + 2), P1 = raw(2 * r0 + 3), P2 = raw(2 * r0 + 4), P3 = raw(2 * r0 + 5);
+    int r = r0;
+    for (; r + 1 < r1; r += 2) {
+        step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
+        step(r + 1, Ic, Id, Ia, Ib, P2, P3, Y, X);
+    }
+    if (r < r1) step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
+}
+
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v3_kernel(uint8_t* stacks, int64_t frame_stride,
+                                                                   int64_t grad_off, int W, int H, int64_t off1, int W1,
+                                                                   int H1, int own, int nstrip, int nband, int first) {
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = blockIdx.x * kL01Waves + wv;
+    if (gw >= nstrip * nband) return;  // (wave-uniform)
+    const int strip = gw % nstrip, band = gw / nstrip;
+    uint8_t* const ibase = stacks + (first + (int64_t)blockIdx.y) * frame_stride;
+    uint8_t* const gbase = ibase + grad_off;
+    const int col0 = 4 * own * strip;
+    const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
+    const bool le = strip == 0, re = col0 + 4 * own >= W;
+    if (le && re) l01v3_strip<true, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else if (le) l01v3_strip<true, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else if (re) l01v3_strip<false, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else l01v3_strip<false, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// pyr_dn_kernel: cv::pyrDown of one level of either stack (levels >= 2), the register-streaming form of
+// pyr_l01v3_kernel without the gradient: lane l takes four source columns, two running sums per lane, two output
+// pixels per lane and output row, unrolled by two so that no register moves.  grid.y = 2 * frames (stack, frame).
+template <bool kLE, bool kRE>
+__device__ __forceinline__ void dn_strip(const uint8_t* src, uint8_t* dst, int W, int H, int W1, int own, int col0,
+                                         int r0, int r1, int lane) {
+    const int c0 = col0 + 4 * (lane - 1);
+    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
+    const bool owner = lane >= 1 && lane <= own;
+    const uint8_t* const lbase = src + cl;
+    auto raw = [&](int y) -> uint32_t {
+        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
+        return *reinterpret_cast<const uint32_t*>(lbase + (ro & ~(int64_t)3));
+    };
+    auto cook = [&](uint32_t lo, int y, uint32_t& e, uint32_t& o) {
+        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
+        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, (uint32_t)(ro & 3));
+        e = pe(v);
+        o = po(v);
+    };
+    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
+        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
+        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
+        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
+        if (kLE && c0 == 0) {
+            A = (A & 0xFFFF0000u) | (C >> 16);
+            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
+        }
+        if (kRE) {
+            const int d = W - 1 - c0;
+            if (d == 0) {
+                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
+                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
+            } else if (d == 1) {
+                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
+            } else if (d == 2) {
+                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
+                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
+            } else if (d == 3) {
+                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
+            }
+        }
+        const u16x2v t = as_u16x2(pk_tap5(A, B, C, D, E)) + (u16x2v){128, 128};
+        const uint32_t q = as_u32(t >> (u16x2v){8, 8});
+        return __builtin_amdgcn_perm(0u, q, 0x0C0C0200u);
+    };
+    const int x = c0 >> 1;
+    const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
+    auto store = [&](int r, uint32_t v) {
+        uint8_t* const d = dst + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
+        if (full_1) *reinterpret_cast<uint16_t*>(d) = (uint16_t)v;
+        if (kRE && part_1) d[0] = (uint8_t)v;
+    };
+    // row r: takes the raw rows 2r + 1, 2r + 2 from Pa, Pb (reloads them with 2r + 5, 2r + 6); X the sums of row r
+    // (stored, then restarted as row r + 2's), Y row r + 1's
+    auto step = [&](int r, uint32_t& Pa, uint32_t& Pb, uint32_t& Xe, uint32_t& Xo, uint32_t& Ye, uint32_t& Yo) {
+        uint32_t e1, o1, e2, o2;
+        cook(Pa, 2 * r + 1, e1, o1);
+        cook(Pb, 2 * r + 2, e2, o2);
+        Pa = raw(2 * r + 5);
+        Pb = raw(2 * r + 6);
+        Xe = pk_add(pk_mad(e1, 4, Xe), e2);
+        Xo = pk_add(pk_mad(o1, 4, Xo), o2);
+        Ye = pk_mad(e2, 6, pk_mad(e1, 4, Ye));
+        Yo = pk_mad(o2, 6, pk_mad(o1, 4, Yo));
+        store(r, hpass2(Xe, Xo));
+        Xe = e2;
+        Xo = o2;
+    };
+    uint32_t Xe, Xo, Ye, Yo;
+    {
+        uint32_t e0, o0, e1, o1, e2, o2;
+        cook(raw(2 * r0 - 2), 2 * r0 - 2, e0, o0);
+        cook(raw(2 * r0 - 1), 2 * r0 - 1, e1, o1);
+        cook(raw(2 * r0), 2 * r0, e2, o2);
+        Xe = pk_mad(e2, 6, pk_mad(e1, 4, e0));
+        Xo = pk_mad(o2, 6, pk_mad(o1, 4, o0));
+        Ye = e2;
+        Yo = o2;
+    }
+    uint32_t P0 = raw(2 * r0 + 1), P1 = raw(2 * r0 + 2), P2 = raw(2 * r0 + 3), P3 = raw(2 * r0 + 4);
+    int r = r0;
+    for (; r + 1 < r1; r += 2) {
+        step(r, P0, P1, Xe, Xo, Ye, Yo);
+        step(r + 1, P2, P3, Ye, Yo, Xe, Xo);
+    }
+    if (r < r1) step(r, P0, P1, Xe, Xo, Ye, Yo);
+}
+
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_dn_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
+                                                                int64_t src_off, int W, int H, int64_t dst_off, int W1,
+                                                                int H1, int own, int nstrip, int nband, int band_rows,
+                                                                int first) {
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = blockIdx.x * kL01Waves + wv;
+    if (gw >= nstrip * nband) return;  // (wave-uniform)
+    const int strip = gw % nstrip, band = gw / nstrip;
+    uint8_t* const base = stacks + (first + (int64_t)(blockIdx.y >> 1)) * frame_stride + ((blockIdx.y & 1) ? grad_off : 0);
+    const int col0 = 4 * own * strip;
+    const int r0 = band * band_rows, r1 = min(r0 + band_rows, H1);
+    const bool le = strip == 0, re = col0 + 4 * own >= W;
+    const uint8_t* const src = base + src_off;
+    uint8_t* const dst = base + dst_off;
+    if (le && re) dn_strip<true, true>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+    else if (le) dn_strip<true, false>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+    else if (re) dn_strip<false, true>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+    else dn_strip<false, false>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+}
+
+int pyr_mode() {  // SVO_PYR: 0 the round-4 kernels, 1 pyr_l01_kernel, 2 pyr_l01v2_kernel, 3 (default) pyr_l01v3_kernel
+    static const int m = getenv("SVO_PYR") ? atoi(getenv("SVO_PYR")) : 3;  // (measurement knob, read once)
     return m;
 }
 
@@ -564,13 +850,27 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
         const int own = (g.w[0] + 4 * nstrip - 1) / (4 * nstrip);
         const int nband = (g.h[1] + kL01Band - 1) / kL01Band;
         const int waves = nstrip * nband;
-        hipLaunchKernelGGL(pyr_mode() == 1 ? pyr_l01_kernel : pyr_l01v2_kernel,
+        hipLaunchKernelGGL(pyr_mode() == 1 ? pyr_l01_kernel : pyr_mode() == 2 ? pyr_l01v2_kernel : pyr_l01v3_kernel,
                            dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count), dim3(64 * kL01Waves), 0, s, stacks,
                            stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1], own, nstrip, nband, first);
         l = 2;
     } else {
         hipLaunchKernelGGL(abs_grad_kernel, dim3((unsigned)((npx + kGradRun - 1) / kGradRun), count), dim3(kGradThreads), 0,
                            s, stacks, stride, grad_off, g.w[0], g.h[0], first);
+    }
+    if (pyr_mode() >= 3) {  // levels >= 2: the streaming pyrDown, both stacks in one launch per level
+        for (; l < g.levels; ++l) {
+            const int w = g.w[l - 1];
+            const int nstrip = (w + 4 * 62 - 1) / (4 * 62);
+            const int own = (w + 4 * nstrip - 1) / (4 * nstrip);
+            // bands of >= 8 output rows, as many as give every frame-stack ~8 waves
+            const int band_rows = max(8, (g.h[l] + 7) / 8);
+            const int nband = (g.h[l] + band_rows - 1) / band_rows;
+            const int waves = nstrip * nband;
+            hipLaunchKernelGGL(pyr_dn_kernel, dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), 2 * count),
+                               dim3(64 * kL01Waves), 0, s, stacks, stride, grad_off, g.off[l - 1], w, g.h[l - 1], g.off[l],
+                               g.w[l], g.h[l], own, nstrip, nband, band_rows, first);
+        }
     }
     for (; l < g.levels; ++l) {
         dim3 grid((g.w[l] + kDnW - 1) / kDnW, (g.h[l] + kDnH - 1) / kDnH, 2 * count);

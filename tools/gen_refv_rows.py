@@ -45,6 +45,8 @@ usage: python3 tools/gen_refv_rows.py [out]  (writes the header; the output is c
 import os
 
 LAYOUTS = (("RowsA", 80), ("RowsB", 72))
+# the quads' instruction-level parallelism form (cls4_ilp / exch_ilp): compares first, then independent per-row chains
+ILP = os.environ.get("SVO_GEN_ILP", "1") == "1"
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "semi-direct-visual-odometry_amd",
                    "csrc", "refv_rows.h")
 
@@ -166,6 +168,8 @@ class Gen:
 
     # ---------------------------------------------------------------- per-quad specializations (namespace scope)
     def cls4(self, q):
+        if ILP:
+            return self.cls4_ilp(q)
         # GE into VCC (e32), LE into a compiler SGPR pair (e64), then the LE mask through VCC by an SALU move: a
         # VALU write of VCC read as a constant by the next VALU needs one wait state (gfx9 "mixed use of VCC"),
         # which the LE compare provides; an SALU write of VCC needs none
@@ -181,7 +185,71 @@ class Gen:
                 f"[a2] \"+v\"(acc[2]), [a3] \"+v\"(acc[3]), [m] \"=&s\"(m)\n                 : [p] \"s\"(p)\n"
                 f"                 : \"vcc\");\n}}\n")
 
+    def cls4_ilp(self, q):
+        # the eight compares of the quad first (e64, into eight compiler-chosen SGPR pairs: independent, they
+        # pipeline), then the sixteen v_writelane by the compiler (their data sources are the pairs' halves, which
+        # the asm operand syntax cannot name: a C++ lane_write per half)
+        rows = list(range(4 * q, 4 * q + 4))
+        L = []
+        for i, r in enumerate(rows):
+            L += [f"v_cmp_ngt_f64_e64 %[g{i}], %[p], {self.reg(r)} ;@vfix 2",
+                  f"v_cmp_nlt_f64_e64 %[l{i}], %[p], {self.reg(r)} ;@vfix 2"]
+        outs = [f'[g{i}] "=&s"(g{i})' for i in range(4)] + [f'[l{i}] "=&s"(l{i})' for i in range(4)]
+        wl = []
+        for i, r in enumerate(rows):
+            ln = r & 63
+            wl += [f"    acc[0] = lane_write(acc[0], (uint32_t)g{i}, {ln}u);",
+                   f"    acc[1] = lane_write(acc[1], (uint32_t)(g{i} >> 32), {ln}u);",
+                   f"    acc[2] = lane_write(acc[2], (uint32_t)l{i}, {ln}u);",
+                   f"    acc[3] = lane_write(acc[3], (uint32_t)(l{i} >> 32), {ln}u);"]
+        return (f"template <> __device__ __forceinline__ void {self.name}::cls4<{q}>(double p, uint32_t (&acc)[4]) {{\n"
+                f"    uint64_t g0, g1, g2, g3, l0, l1, l2, l3;\n"
+                f"    asm volatile(\"{asm(L)}\"\n                 : {', '.join(outs)}\n                 : [p] \"s\"(p));\n"
+                + "\n".join(wl) + "\n}\n")
+
+    def exch_ilp(self, q, side, write, edge, nr=4):
+        # block 1: the rows' compares; (edge forms) the rows outside [ra, ra + len] drop their masks (scalar selects);
+        # block 2: every row's slot address first (readlane of the row's base, mbcnt over the mask's halves: nr
+        # independent chains that pipeline), then the exec-masked LDS accesses, the reads all in flight together
+        rows = list(range(nr * q, nr * q + nr))
+        cmp = "v_cmp_nlt_f64" if side == 0 else "v_cmp_ngt_f64"
+        L1 = [f"{cmp} %[m{i}], {self.reg(r)}, %[p] ;@vfix 1" for i, r in enumerate(rows)]
+        L2 = ["s_nop 0"]  # (a VALU write of pb just before the block -> v_readlane of it: one wait state)
+        L2 += [f"v_readlane_b32 %[t{i}], %[pb], {r & 63}" for i, r in enumerate(rows)]
+        L2 += [f"v_mbcnt_lo_u32_b32 %[k{i}], %[ml{i}], 0" for i in range(nr)]
+        L2 += [f"v_mbcnt_hi_u32_b32 %[k{i}], %[mh{i}], %[k{i}]" for i in range(nr)]
+        L2 += [(f"v_lshl_add_u32 %[k{i}], %[k{i}], 3, %[t{i}]" if side == 0 else f"v_mad_i32_i24 %[k{i}], %[k{i}], -8, %[t{i}]")
+               for i in range(nr)]
+        L2.append("s_mov_b64 %[sv], exec")
+        for i, r in enumerate(rows):
+            L2 += [f"s_mov_b64 exec, %[m{i}]",
+                   f"ds_write_b64 %[k{i}], {self.reg(r)} ;@vfix 1" if write else f"ds_read_b64 %[x{i}], %[k{i}]"]
+        if not write:
+            L2.append("s_waitcnt lgkmcnt(0)")
+            for i, r in enumerate(rows):
+                L2 += [f"s_mov_b64 exec, %[m{i}]", f"v_mov_b64 {self.reg(r)}, %[x{i}] ;@vfix 0"]
+        L2.append("s_mov_b64 exec, %[sv]")
+        mdecl = ", ".join(f"m{i}" for i in range(nr))
+        decl = f"uint64_t {mdecl}, sv;\n    uint32_t " + ", ".join(f"t{i}, k{i}" for i in range(nr)) + ";\n"
+        outs2 = ['[sv] "=&s"(sv)'] + [f'[t{i}] "=&s"(t{i})' for i in range(nr)] + [f'[k{i}] "=&v"(k{i})' for i in range(nr)]
+        if not write:
+            decl += "    uint64_t " + ", ".join(f"x{i}" for i in range(nr)) + ";\n"
+            outs2 += [f'[x{i}] "=&v"(x{i})' for i in range(nr)]
+        ins2 = ['[pb] "v"(pb)'] + [f'[m{i}] "s"(m{i})' for i in range(nr)] + \
+               [f'[ml{i}] "s"((uint32_t)m{i})' for i in range(nr)] + [f'[mh{i}] "s"((uint32_t)(m{i} >> 32))' for i in range(nr)]
+        outs1 = ", ".join(f'[m{i}] "=&s"(m{i})' for i in range(nr))
+        edge_c = "".join(f"    if ({r}u - ra > len) m{i} = 0;\n" for i, r in enumerate(rows)) if edge else ""
+        name = ("src" if write else "tgt") + str(nr) + ("e" if edge else "")
+        args = "double p, uint32_t pb" + (", uint32_t ra, uint32_t len" if edge else "")
+        return (f"template <> __device__ __forceinline__ void {self.name}::{name}<{q}, {side}>({args}) {{\n    {decl}"
+                f"    asm volatile(\"{asm(L1)}\"\n                 : {outs1}\n"
+                f"                 : [p] \"s\"(p));\n{edge_c}"
+                f"    asm volatile(\"{asm(L2)}\"\n                 : {', '.join(outs2)}\n                 : {', '.join(ins2)}\n"
+                f"                 : \"memory\", \"scc\");\n}}\n")
+
     def exch(self, q, side, write, edge, nr=4):
+        if ILP:
+            return self.exch_ilp(q, side, write, edge, nr)
         rows = list(range(nr * q, nr * q + nr))
         cmp = "v_cmp_nlt_f64" if side == 0 else "v_cmp_ngt_f64"
         L = ["s_mov_b64 %[sv], exec"]
