@@ -748,7 +748,14 @@ __device__ __forceinline__ void dn_strip(const uint8_t* src, uint8_t* dst, int W
             A = (A & 0xFFFF0000u) | (C >> 16);
             B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
         }
-        if (kRE) {
+        if (kLE && kRE && W <= 2) {  // one or two columns: every tap reflects back into them (x0 only: W1 = 1)
+            const uint32_t v0 = C & 0xFFFFu, v1 = W == 2 ? (D & 0xFFFFu) : v0;
+            A = v0;
+            B = v1;
+            C = v0;
+            D = v1;
+            E = v0;
+        } else if (kRE) {
             const int d = W - 1 - c0;
             if (d == 0) {
                 D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
