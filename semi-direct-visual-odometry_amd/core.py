@@ -10,6 +10,7 @@ plus the batched forms the GPU is built for (AlignBatch, FeatureAlignment.align_
 """
 import ctypes
 import math
+import operator
 import time
 
 import numpy as np
@@ -303,6 +304,7 @@ class Feature:
         self.type = feature_type
         self._bearing = None if bearing is None else np.asarray(bearing, np.float64)
         self._point = point
+        self._pi = -1 if point is None else point._i  # the point's _PT row (-1: none), read by the array gathers
         self._touch()
 
     @classmethod
@@ -318,8 +320,10 @@ class Feature:
         new = object.__new__
         for i in range(n):
             f = new(cls)
+            p = pts[i]
             f.__dict__ = {"_frame": frame, "_px": pxf[i], "level": level, "gradient_magnitude": gm[i],
-                          "gradient_orientation": 0.0, "type": feature_type, "_bearing": None, "_point": pts[i]}
+                          "gradient_orientation": 0.0, "type": feature_type, "_bearing": None, "_point": p,
+                          "_pi": -1 if p is None else p._i}
             out.append(f)
         return out
 
@@ -357,6 +361,7 @@ class Feature:
     @point.setter
     def point(self, p):
         self._point = p
+        self._pi = -1 if p is None else p._i
         self._touch()
 
     @property
@@ -472,9 +477,13 @@ def _rows(vals, width):
     return np.array(vals, dtype=np.float64).reshape(n, width)
 
 
+_get_pi = operator.attrgetter("_pi")
+
+
 def _point_rows(feats):
-    """The _PT rows of the features' points (-1: no point)."""
-    return np.fromiter((-1 if f._point is None else f._point._i for f in feats), np.int64, count=len(feats))
+    """The _PT rows of the features' points (-1: no point).  A live point's row is never reused (the feature
+    holds the point), so each Feature keeps it in _pi."""
+    return np.fromiter(map(_get_pi, feats), np.int64, count=len(feats))
 
 
 def _gather_points(idx):
@@ -772,15 +781,19 @@ class Map:
         if ref_frame.last_keyframe is None:
             raise ValueError("reprojectMap needs refFrame->m_lastKeyframe")
         kfs = [ref_frame, ref_frame.last_keyframe]
-        feats = [f for kf in kfs for f in kf.features]
-        off = np.cumsum([0] + [len(kf.features) for kf in kfs]).astype(np.int32)
-        # the distinct points in first-seen order (a Point hashes by identity) and each feature's index among them
-        pts = [f._point for f in feats]
-        points = list(dict.fromkeys(p for p in pts if p is not None))
-        row_of = dict(zip(points, range(len(points))))
-        feat_point = np.array([row_of.get(p, -1) for p in pts] or [-1], np.int32)
-        npt = len(points)
-        prow = np.fromiter((p._i for p in points), np.int64, count=npt)
+        nfs = [len(kf.features) for kf in kfs]
+        off = np.cumsum([0] + nfs).astype(np.int32)
+        # the distinct points (their _PT rows) in first-seen order and each feature's index among them (-1: none)
+        rows = np.concatenate([_point_rows(kf.features) for kf in kfs])
+        valid = rows >= 0
+        u, first, inv = np.unique(rows[valid], return_index=True, return_inverse=True)
+        order = np.argsort(first, kind="stable")
+        prow = u[order]
+        rank = np.empty(len(u), np.int32)
+        rank[order] = np.arange(len(u), dtype=np.int32)
+        feat_point = np.full(max(len(rows), 1), -1, np.int32)
+        feat_point[np.nonzero(valid)[0]] = rank[inv.reshape(-1)]
+        npt = len(prow)
         pos = np.ascontiguousarray(_PT.pos[prow]) if npt else np.zeros((1, 3))
         ptype = _PT.type[prow] if npt else np.zeros(1, np.uint32)
         plast = _PT.last[prow] if npt else np.zeros(1, np.uint64)
@@ -804,7 +817,9 @@ class Map:
             overlap_keyframes.append((kf, int(overlap[k])))
         self.matches, self.trials = m.value, t.value
         ns = n_sel.value
-        chosen = [feats[i] for i in sel_feat[:ns]]
+        f0, f1 = kfs[0].features, kfs[1].features
+        n0 = nfs[0]
+        chosen = [f0[i] if i < n0 else f1[i - n0] for i in sel_feat[:ns].tolist()]
         px = np.ascontiguousarray(sel_px[:ns])
         t0 = time.perf_counter()
         self.alignment.align_many(chosen, cur_frame, px)

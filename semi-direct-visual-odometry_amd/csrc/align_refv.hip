@@ -124,14 +124,13 @@ constexpr uint32_t kTrHead = 8;
 [[maybe_unused]] constexpr bool kStampsSmall = false;
 #endif
 #if defined(SVO_STAMPS) && defined(SVO_STAMPS_WAVES)
+// (the wave's sums stay in scalar registers, phacc, and reach dg at the end of each pass: no memory traffic and no
+// vector registers inside the rounds)
 #define VSTAMP(i) \
     do { \
-        if (kStampOn && dg && lane == 0) { \
+        if (kStampOn && dg) { \
             const uint64_t t_ = clock64(); \
-            if (!kStampsSmall || small_round) { \
-                dg->phw[wave][i] += (uint32_t)(t_ - tstamp); \
-                if (tid == 0) dg->ph[i] += t_ - tstamp; \
-            } \
+            if (!kStampsSmall || small_round) phacc[i] += (uint32_t)(t_ - tstamp); \
             tstamp = t_; \
         } \
     } while (0)
@@ -208,6 +207,9 @@ struct VSel {
     double lo_val;
     int P;
     bool small_round = false;  // (stamps build: the current block round has < 2048 positions)
+#if defined(SVO_STAMPS) && defined(SVO_STAMPS_WAVES)
+    uint32_t phacc[12] = {};  // (stamps build, per wave: cycles per phase of this pass so far)
+#endif
 
     // ------------------------------------------------------------------ registers
     // body(r, x) for this wave's rows rlo..rhi, x the lane's value (kWrite: body may change it)
@@ -702,10 +704,18 @@ struct VSel {
         asm volatile("" : "+v"(tid), "+v"(lane));
         wave = (int)uni((uint32_t)tid >> 6);
     }
-    // the round trace (debug kernel only: dg->tr set)
+    // the round trace (debug kernel only: dg->tr set; compiled out of the stamps build, whose clock reads need the
+    // registers the trace code holds)
+    __device__ __forceinline__ bool tracing() const {
+#if defined(SVO_STAMPS)
+        return false;
+#else
+        return dg && dg->tr;
+#endif
+    }
     __device__ __forceinline__ double* trace_rec(uint32_t kind, uint32_t f0, uint32_t l0, double p, uint32_t ks,
                                                  uint32_t tg, uint32_t tl, uint32_t cut) {
-        if (!dg || !dg->tr) return nullptr;
+        if (!tracing()) return nullptr;
         const uint32_t i = dg->ntr;
         if ((uint64_t)(i + 1u) * (kTrHead + M) > dg->trcap) return nullptr;
         double* const b = dg->tr + (uint64_t)i * (kTrHead + M);
@@ -726,7 +736,7 @@ struct VSel {
             });
         }
         __syncthreads();
-        if (dg && dg->tr && tid == 0) ++dg->ntr;
+        if (tracing() && tid == 0) ++dg->ntr;
         __syncthreads();
     }
     __device__ __forceinline__ void block_round(double p, uint32_t ch, double x0, double (&cand)[4]) {
@@ -850,7 +860,7 @@ struct VSel {
             ++dg->nlog;
         }
 #endif
-        if (dg && dg->tr) {
+        if (tracing()) {
             const uint32_t f0 = f, l0 = l;
             f = nf;
             l = nl;
@@ -957,7 +967,7 @@ struct VSel {
                     if (je >= 4) G::template w1tgt<1, 0>(acc[0], acc[1], pkv, ks, tl1, mbb);
                 }
             }
-            if (dg && dg->tr) {  // (wave 0 only: no barrier; the record counter is wave 0's)
+            if (tracing()) {  // (wave 0 only: no barrier; the record counter is wave 0's)
                 double* const v = trace_rec(1, f0 + fr, f0 + lr, pe, ks, tG, tL, f0 + cut);
                 if (v) {
 #pragma unroll
@@ -1025,7 +1035,7 @@ struct VSel {
                 x = __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
                 asm volatile("" ::: "memory");
             }
-            if (dg && dg->tr) {
+            if (tracing()) {
                 double* const v = trace_rec(1, f0 + w + a, f0 + w + b, pe, ks, tG, tL, f0 + w + cut);
                 if (v) {
                     if (me < n0) v[f0 + w + me] = x;
@@ -1121,6 +1131,16 @@ struct VSel {
         // reaches after these reads have completed)
         if (did_preload && wave == 0) unstage_wave0();
         VSTAMP(7);
+#if defined(SVO_STAMPS) && defined(SVO_STAMPS_WAVES)
+        if (kStampOn && dg && lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+                dg->phw[wave][i] += phacc[i];
+                if (tid == 0) dg->ph[i] += phacc[i];
+                phacc[i] = 0;
+            }
+        }
+#endif
         if (dg && tid == 0) {
             dg->nblock[P] = nblock;
             dg->cyc[P] = clock64() - t0;

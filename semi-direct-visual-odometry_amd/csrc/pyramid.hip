@@ -556,7 +556,7 @@ __device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t k, uint32_t c) {
     return as_u32(as_u16x2(a) * (u16x2v){(uint16_t)k, (uint16_t)k} + as_u16x2(c));
 }
 
-template <bool kLE, bool kRE>
+template <bool kLE, bool kRE, int kD, int kX = 0>
 __device__ __forceinline__ void l01v3_strip(uint8_t* ibase, uint8_t* gbase, int W, int H, int64_t off1, int W1, int own,
                                             int col0, int r0, int r1, int lane) {
     const int c0 = col0 + 4 * (lane - 1);
@@ -635,30 +635,57 @@ __device__ __forceinline__ void l01v3_strip(uint8_t* ibase, uint8_t* gbase, int 
     auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
         if (y >= ylim) return;  // (uniform)
         const uint32_t v = ge | (go << 8);
-        uint8_t* const d = gbase + (int64_t)__builtin_amdgcn_readfirstlane(y * W) + c0;
+        if (kX == 3) {  // aligned dwords: the lane stores columns c0 - s .. c0 - s + 3 (s: the row's misalignment)
+            const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(y * W);
+            const uint32_t sh = (uint32_t)ro & 3u;
+            const uint32_t w = __builtin_amdgcn_perm(v, from_left(v), 0x07060504u - sh * 0x01010101u);
+            uint8_t* const da = gbase + (ro - (int64_t)sh) + c0;
+            const int lo = c0 - (int)sh;  // the dword's first column
+            if (!kLE && !kRE) {
+                if (owner) *reinterpret_cast<uint32_t*>(da) = w;
+            } else {
+                // (edge strips: the strip's first dword starts before column 0, the last one runs past W - 1: those
+                // lanes store their row's bytes one by one; the lane after the last owner carries its tail)
+                const bool any = lane >= 1 && lo <= W - 1 && lane <= (kRE ? own + 1 : own);
+                if (any && lo >= 0 && lo + 3 <= W - 1) *reinterpret_cast<uint32_t*>(da) = w;
+                else if (any)
+                    for (int i = 0; i < 4; ++i)
+                        if (lo + i >= 0 && lo + i <= W - 1) da[i] = (uint8_t)(w >> (8 * i));
+            }
+            return;
+        }
+        uint8_t* d = gbase + (int64_t)__builtin_amdgcn_readfirstlane(y * W) + c0;
+        if (kX == 1) d = (uint8_t*)((uintptr_t)d & ~(uintptr_t)3);  // (timing experiment only: wrong bytes)
+        if (kX == 2) return;
         if (full_g) *reinterpret_cast<uint32_t*>(d) = v;
         if (kRE && part_g)
             for (int i = 0; i < 4; ++i)
                 if (c0 + i < W) d[i] = (uint8_t)(v >> (8 * i));
     };
     auto store_l1 = [&](uint8_t* plane, int r, uint32_t v) {
-        uint8_t* const d = plane + off1 + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
+        uint8_t* d = plane + off1 + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
+        if (kX == 1) d = (uint8_t*)((uintptr_t)d & ~(uintptr_t)1);
+        if (kX == 2) {  // (keep the value live)
+            asm volatile("" ::"v"(v));
+            return;
+        }
         if (full_1) *reinterpret_cast<uint16_t*>(d) = (uint16_t)v;
         if (kRE && part_1) d[0] = (uint8_t)v;
     };
     // one level-1 row r: holds I(2r), I(2r + 1) in I0, I1, takes the raw rows 2r + 2, 2r + 3 from Pa, Pb (reloads
-    // them with 2r + 6, 2r + 7), leaves I(2r + 2), I(2r + 3) in I2, I3; X: the sums of row r (completed and stored
+    // them with the rows kD steps ahead, 2r + 2 + 2kD and 2r + 3 + 2kD), leaves I(2r + 2), I(2r + 3) in I2, I3; X: the sums of row r (completed and stored
     // here, then restarted as row r + 2's), Y: row r + 1's
     auto step = [&](int r, const Px4& I0, const Px4& I1, Px4& I2, Px4& I3, uint32_t& Pa, uint32_t& Pb, Acc& X, Acc& Y) {
         I2 = cook(Pa, 2 * r + 2);
         I3 = cook(Pb, 2 * r + 3);
-        Pa = raw(2 * r + 6);
-        Pb = raw(2 * r + 7);
+        Pa = raw(2 * r + 2 + 2 * kD);
+        Pb = raw(2 * r + 3 + 2 * kD);
         uint32_t g1e, g1o, g2e, g2o;
         grad(I0, I1, I2, 2 * r + 1, g1e, g1o);
         grad(I1, I2, I3, 2 * r + 2, g2e, g2o);
         store_grad(2 * r + 1, g1e, g1o);
         store_grad(2 * r + 2, g2e, g2o);
+        if (kX == 2) asm volatile("" ::"v"(g1e), "v"(g1o), "v"(g2e), "v"(g2o));
         // row 2r + 1: 4x into rows r and r + 1; row 2r + 2: 1x into r (complete), 6x into r + 1, 1x starts r + 2
         X.ie = pk_add(pk_mad(I1.e, 4, X.ie), I2.e);
         X.io = pk_add(pk_mad(I1.o, 4, X.io), I2.o);
@@ -692,15 +719,27 @@ __device__ __forceinline__ void l01v3_strip(uint8_t* ibase, uint8_t* gbase, int 
         X.go = pk_mad(h0o, 6, pk_mad(hm1o, 4, hm2o));
         Y = Acc{Ia.e, Ia.o, h0e, h0o};
     }
-    uint32_t P0 = raw(2 * r0 + 2), P1 = raw(2 * r0 + 3), P2 = raw(2 * r0 + 4), P3 = raw(2 * r0 + 5);
+    // kD steps of raw rows in flight; the loop unrolled by kD (even) so that every role keeps its registers
+    static_assert(kD % 2 == 0, "the running sums alternate between two register sets");
+    uint32_t P[2 * kD];
+#pragma unroll
+    for (int k = 0; k < 2 * kD; ++k) P[k] = raw(2 * r0 + 2 + k);
     int r = r0;
-    for (; r + 1 < r1; r += 2) {
-        step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
-        step(r + 1, Ic, Id, Ia, Ib, P2, P3, Y, X);
+    for (; r + kD - 1 < r1; r += kD) {
+#pragma unroll
+        for (int i = 0; i < kD; i += 2) {
+            step(r + i, Ia, Ib, Ic, Id, P[2 * i], P[2 * i + 1], X, Y);
+            step(r + i + 1, Ic, Id, Ia, Ib, P[2 * i + 2], P[2 * i + 3], Y, X);
+        }
     }
-    if (r < r1) step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
+#pragma unroll
+    for (int i = 0; i < kD; i += 2) {  // the band's last r1 - r < kD rows (uniform)
+        if (r + i < r1) step(r + i, Ia, Ib, Ic, Id, P[2 * i], P[2 * i + 1], X, Y);
+        if (r + i + 1 < r1) step(r + i + 1, Ic, Id, Ia, Ib, P[2 * i + 2], P[2 * i + 3], Y, X);
+    }
 }
 
+template <int kD, int kX = 0>
 __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v3_kernel(uint8_t* stacks, int64_t frame_stride,
                                                                    int64_t grad_off, int W, int H, int64_t off1, int W1,
                                                                    int H1, int own, int nstrip, int nband, int first) {
@@ -713,17 +752,248 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v3_kernel(uint8_t* stac
     const int col0 = 4 * own * strip;
     const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
     const bool le = strip == 0, re = col0 + 4 * own >= W;
-    if (le && re) l01v3_strip<true, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else if (le) l01v3_strip<true, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else if (re) l01v3_strip<false, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else l01v3_strip<false, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    if (le && re) l01v3_strip<true, true, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else if (le) l01v3_strip<true, false, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else if (re) l01v3_strip<false, true, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+    else l01v3_strip<false, false, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// pyr_l01v4_kernel: pyr_l01v3's pass with fewer VALU per step (the profile of v3: VALU ~2/3 busy, the texture
+// addresser ~3/4 busy):
+//  * the horizontal gradient in the pair domain: the left / right neighbours of columns (0, 2) are (-1, 1) / (1, 3)
+//    and of (1, 3) are (0, 2) / (2, 4): one DPP and one alignbyte per parity instead of two DPPs, two alignbytes
+//    and four byte permutes on the unpacked row;
+//  * the running sums' 4x terms as v_pk_mad_u16 (the compiler's choice was a shift and an add);
+//  * the rounding shift of the horizontal pass folded into the final byte permute (the high bytes of sum + 128);
+//  * bands that touch neither the first nor the last base rows (kIn) carry no row reflection and no border-row test;
+//  * (kAl) the level-0 gradient leaves as aligned dwords: the lane stores columns c0 - s .. c0 - s + 3 of its row (s the
+//    row's misalignment), the bytes of the left lane's last s columns by one DPP and one permute; the lanes whose
+//    dword leaves the row store bytes.
+__device__ __forceinline__ uint32_t pk_mad4(uint32_t a, uint32_t c) {  // a * 4 + c on u16 pairs, one instruction
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_mad6(uint32_t a, uint32_t c) {
+    uint32_t r;
+    asm("v_pk_mad_u16 %0, %1, 6, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(c));
+    return r;
+}
+struct Px2 {
+    uint32_t e, o;  // columns (0, 2) and (1, 3) as u16 pairs
+};
+
+template <bool kLE, bool kRE, bool kIn, bool kAl, bool kW = false>
+__device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int32_t stack_bytes, int W, int H, int64_t off1,
+                                            int W1, int own, int col0, int r0, int r1, int lane) {
+    const int c0 = col0 + 4 * (lane - 1);
+    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
+    const bool owner = lane >= 1 && lane <= own;
+    uint32_t me = 0xFFFFFFFFu, mo = 0xFFFFFFFFu;
+    if (kLE && c0 == 0) me &= 0xFFFF0000u;
+    if (kRE) {
+        if (c0 == W - 1) me &= 0xFFFF0000u;
+        if (c0 + 2 == W - 1) me &= 0x0000FFFFu;
+        if (c0 + 1 == W - 1) mo &= 0xFFFF0000u;
+        if (c0 + 3 == W - 1) mo &= 0x0000FFFFu;
+    }
+    // (buffer accesses: the stack in a descriptor, the row offset a scalar, the lane's column the vector offset; no
+    // 64-bit address arithmetic per lane and access)
+    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(ibase, 0, stack_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(gbase, 0, stack_bytes, 0x00020000);
+    const uint32_t ucl = (uint32_t)cl, uc0 = (uint32_t)c0, ux = (uint32_t)(c0 >> 1);
+    auto prow = [&](int y) -> int64_t {  // (uniform) the base offset of image row y
+        return kIn ? (int64_t)__builtin_amdgcn_readfirstlane(y) * W
+                   : (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
+    };
+    auto raw = [&](int y) -> uint32_t {
+        return __builtin_amdgcn_raw_buffer_load_b32(ri, ucl, (uint32_t)(prow(y) & ~(int64_t)3), 0);
+    };
+    auto cook = [&](uint32_t lo, int y) -> Px2 {
+        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, (uint32_t)(prow(y) & 3));
+        return Px2{pe(v), po(v)};
+    };
+    auto grad = [&](const Px2& up, const Px2& mid, const Px2& dn, int y, uint32_t& ge, uint32_t& go) {
+        const uint32_t le = __builtin_amdgcn_alignbyte(mid.o, from_left(mid.o), 2);   // columns (-1, 1)
+        const uint32_t ro = __builtin_amdgcn_alignbyte(from_right(mid.e), mid.e, 2);  // columns (2, 4)
+        const u16x2v lim = {255, 255};
+        ge = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(le, mid.o), pk_absdiff(up.e, dn.e))), lim));
+        go = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(mid.e, ro), pk_absdiff(up.o, dn.o))), lim));
+        if (!kIn) {
+            const int py = __builtin_amdgcn_readfirstlane(refl101(y, H));
+            if (py == 0 || py == H - 1) {  // (uniform)
+                ge = 0u;
+                go = 0u;
+            }
+        }
+        if (kLE || kRE) {
+            ge &= me;
+            go &= mo;
+        }
+    };
+    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
+        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
+        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
+        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
+        if (kLE && c0 == 0) {
+            A = (A & 0xFFFF0000u) | (C >> 16);
+            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
+        }
+        if (kRE) {
+            const int d = W - 1 - c0;
+            if (d == 0) {
+                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
+                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
+            } else if (d == 1) {
+                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
+            } else if (d == 2) {
+                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
+                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
+            } else if (d == 3) {
+                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
+            }
+        }
+        // (A + E) + 4 (B + D) + 6 C + 128, every partial below 2^16; the outputs are the pairs' high bytes
+        const uint32_t t = pk_mad6(C, pk_mad4(pk_add(B, D), pk_add(A, E)));
+        const uint32_t q = as_u32(as_u16x2(t) + (u16x2v){128, 128});
+        return __builtin_amdgcn_perm(0u, q, 0x0C0C0301u);  // x0 | x1 << 8
+    };
+    const bool full_g = owner && (!kRE || c0 + 3 < W), part_g = kRE && owner && c0 < W && c0 + 3 >= W;
+    const int x = c0 >> 1;
+    const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
+    const int ylim = min(2 * r1, H);
+    auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
+        if (y >= ylim) return;  // (uniform)
+        const uint32_t v = ge | (go << 8);
+        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(y * W);
+        if (kAl) {
+            const uint32_t sh = (uint32_t)ro & 3u;
+            const uint32_t w = __builtin_amdgcn_perm(v, from_left(v), 0x07060504u - sh * 0x01010101u);
+            const uint32_t so = (uint32_t)(ro - (int64_t)sh);
+            const int lo = c0 - (int)sh;  // the dword's first column
+            if (!kLE && !kRE) {
+                if (owner) __builtin_amdgcn_raw_buffer_store_b32(w, rg, uc0, so, 0);
+            } else {
+                const bool any = lane >= 1 && lo <= W - 1 && lane <= (kRE ? own + 1 : own);
+                if (any && lo >= 0 && lo + 3 <= W - 1) __builtin_amdgcn_raw_buffer_store_b32(w, rg, uc0, so, 0);
+                else if (any)
+                    for (int i = 0; i < 4; ++i)
+                        if (lo + i >= 0 && lo + i <= W - 1)
+                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8 * i)), rg, uc0 + (uint32_t)i, so, 0);
+            }
+            return;
+        }
+        if (kW) {  // (timing experiment: 16-B stores from every fourth lane, the quad's dwords by DPP; strip-edge bytes wrong)
+            const uint32_t g1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xF, 0xF, true);
+            const uint32_t g2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x102, 0xF, 0xF, true);
+            const uint32_t g3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x103, 0xF, 0xF, true);
+            typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+            if (owner && (lane & 3) == 0 && c0 + 15 < W)
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4v){v, g1, g2, g3}, rg, uc0, (uint32_t)ro, 0);
+            return;
+        }
+        if (full_g) __builtin_amdgcn_raw_buffer_store_b32(v, rg, uc0, (uint32_t)ro, 0);
+        if (kRE && part_g)
+            for (int i = 0; i < 4; ++i)
+                if (c0 + i < W) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(v >> (8 * i)), rg, uc0 + (uint32_t)i, (uint32_t)ro, 0);
+    };
+    auto store_l1 = [&](const __amdgpu_buffer_rsrc_t& rs, int r, uint32_t v) {
+        const uint32_t so = (uint32_t)off1 + (uint32_t)__builtin_amdgcn_readfirstlane(r * W1);
+        if (kW) {
+            const uint32_t d = (v & 0xFFFFu) | (from_right(v) << 16);
+            const uint32_t d2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0x102, 0xF, 0xF, true);
+            const uint32_t d4 = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0x104, 0xF, 0xF, true);
+            const uint32_t d6 = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0x106, 0xF, 0xF, true);
+            typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+            if (owner && (lane & 7) == 0 && (int)ux + 15 < W1)
+                __builtin_amdgcn_raw_buffer_store_b128((u32x4v){d, d2, d4, d6}, rs, ux, so, 0);
+            return;
+        }
+        if (full_1) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
+        if (kRE && part_1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, rs, ux, so, 0);
+    };
+    auto step = [&](int r, const Px2& I0, const Px2& I1, Px2& I2, Px2& I3, uint32_t& Pa, uint32_t& Pb, Acc& X, Acc& Y) {
+        I2 = cook(Pa, 2 * r + 2);
+        I3 = cook(Pb, 2 * r + 3);
+        Pa = raw(2 * r + 6);
+        Pb = raw(2 * r + 7);
+        uint32_t g1e, g1o, g2e, g2o;
+        grad(I0, I1, I2, 2 * r + 1, g1e, g1o);
+        grad(I1, I2, I3, 2 * r + 2, g2e, g2o);
+        store_grad(2 * r + 1, g1e, g1o);
+        store_grad(2 * r + 2, g2e, g2o);
+        X.ie = pk_add(pk_mad4(I1.e, X.ie), I2.e);
+        X.io = pk_add(pk_mad4(I1.o, X.io), I2.o);
+        X.ge = pk_add(pk_mad4(g1e, X.ge), g2e);
+        X.go = pk_add(pk_mad4(g1o, X.go), g2o);
+        Y.ie = pk_mad6(I2.e, pk_mad4(I1.e, Y.ie));
+        Y.io = pk_mad6(I2.o, pk_mad4(I1.o, Y.io));
+        Y.ge = pk_mad6(g2e, pk_mad4(g1e, Y.ge));
+        Y.go = pk_mad6(g2o, pk_mad4(g1o, Y.go));
+        store_l1(ri, r, hpass2(X.ie, X.io));
+        store_l1(rg, r, hpass2(X.ge, X.go));
+        X = Acc{I2.e, I2.o, g2e, g2o};
+    };
+    Px2 Ia, Ib, Ic, Id;
+    Acc X, Y;
+    {
+        const Px2 Jm3 = cook(raw(2 * r0 - 3), 2 * r0 - 3), Jm2 = cook(raw(2 * r0 - 2), 2 * r0 - 2);
+        const Px2 Jm1 = cook(raw(2 * r0 - 1), 2 * r0 - 1);
+        Ia = cook(raw(2 * r0), 2 * r0);
+        Ib = cook(raw(2 * r0 + 1), 2 * r0 + 1);
+        uint32_t hm2e, hm2o, hm1e, hm1o, h0e, h0o;
+        grad(Jm3, Jm2, Jm1, 2 * r0 - 2, hm2e, hm2o);
+        grad(Jm2, Jm1, Ia, 2 * r0 - 1, hm1e, hm1o);
+        grad(Jm1, Ia, Ib, 2 * r0, h0e, h0o);
+        store_grad(2 * r0, h0e, h0o);
+        X.ie = pk_mad6(Ia.e, pk_mad4(Jm1.e, Jm2.e));
+        X.io = pk_mad6(Ia.o, pk_mad4(Jm1.o, Jm2.o));
+        X.ge = pk_mad6(h0e, pk_mad4(hm1e, hm2e));
+        X.go = pk_mad6(h0o, pk_mad4(hm1o, hm2o));
+        Y = Acc{Ia.e, Ia.o, h0e, h0o};
+    }
+    uint32_t P0 = raw(2 * r0 + 2), P1 = raw(2 * r0 + 3), P2 = raw(2 * r0 + 4), P3 = raw(2 * r0 + 5);
+    int r = r0;
+    for (; r + 1 < r1; r += 2) {
+        step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
+        step(r + 1, Ic, Id, Ia, Ib, P2, P3, Y, X);
+    }
+    if (r < r1) step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
+}
+
+template <bool kAl, bool kW = false>
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v4_kernel(uint8_t* stacks, int64_t frame_stride,
+                                                                   int64_t grad_off, int W, int H, int64_t off1, int W1,
+                                                                   int H1, int own, int nstrip, int nband, int first) {
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = blockIdx.x * kL01Waves + wv;
+    if (gw >= nstrip * nband) return;  // (wave-uniform)
+    const int strip = gw % nstrip, band = gw / nstrip;
+    uint8_t* const ibase = stacks + (first + (int64_t)blockIdx.y) * frame_stride;
+    uint8_t* const gbase = ibase + grad_off;
+    const int col0 = 4 * own * strip;
+    const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
+    const bool le = strip == 0, re = col0 + 4 * own >= W;
+    // the band's rows 2 r0 - 3 .. 2 r1 + 7 (reads, the prefetch included) and its gradient rows 2 r0 - 2 .. 2 r1 all
+    // inside [1, H - 2]: no reflection, no border row
+    const bool in = 2 * r0 - 3 >= 1 && 2 * r1 + 7 <= H - 2;
+    const int32_t sb = (int32_t)grad_off;  // (each stack's bytes fit below the gradient stack's offset)
+#define SVO_L01V4(LE, RE)                                                                                   \
+    if (in) l01v4_strip<LE, RE, true, kAl, kW>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);      \
+    else l01v4_strip<LE, RE, false, kAl, kW>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);
+    if (le && re) { SVO_L01V4(true, true) }
+    else if (le) { SVO_L01V4(true, false) }
+    else if (re) { SVO_L01V4(false, true) }
+    else { SVO_L01V4(false, false) }
+#undef SVO_L01V4
 }
 
 // ---------------------------------------------------------------------------------------------------------------
 // pyr_dn_kernel: cv::pyrDown of one level of either stack (levels >= 2), the register-streaming form of
 // pyr_l01v3_kernel without the gradient: lane l takes four source columns, two running sums per lane, two output
 // pixels per lane and output row, unrolled by two so that no register moves.  grid.y = 2 * frames (stack, frame).
-template <bool kLE, bool kRE>
+template <bool kLE, bool kRE, int kD>
 __device__ __forceinline__ void dn_strip(const uint8_t* src, uint8_t* dst, int W, int H, int W1, int own, int col0,
                                          int r0, int r1, int lane) {
     const int c0 = col0 + 4 * (lane - 1);
@@ -786,8 +1056,8 @@ __device__ __forceinline__ void dn_strip(const uint8_t* src, uint8_t* dst, int W
         uint32_t e1, o1, e2, o2;
         cook(Pa, 2 * r + 1, e1, o1);
         cook(Pb, 2 * r + 2, e2, o2);
-        Pa = raw(2 * r + 5);
-        Pb = raw(2 * r + 6);
+        Pa = raw(2 * r + 1 + 2 * kD);
+        Pb = raw(2 * r + 2 + 2 * kD);
         Xe = pk_add(pk_mad(e1, 4, Xe), e2);
         Xo = pk_add(pk_mad(o1, 4, Xo), o2);
         Ye = pk_mad(e2, 6, pk_mad(e1, 4, Ye));
@@ -807,15 +1077,26 @@ __device__ __forceinline__ void dn_strip(const uint8_t* src, uint8_t* dst, int W
         Ye = e2;
         Yo = o2;
     }
-    uint32_t P0 = raw(2 * r0 + 1), P1 = raw(2 * r0 + 2), P2 = raw(2 * r0 + 3), P3 = raw(2 * r0 + 4);
+    static_assert(kD % 2 == 0, "the running sums alternate between two register sets");
+    uint32_t P[2 * kD];
+#pragma unroll
+    for (int k = 0; k < 2 * kD; ++k) P[k] = raw(2 * r0 + 1 + k);
     int r = r0;
-    for (; r + 1 < r1; r += 2) {
-        step(r, P0, P1, Xe, Xo, Ye, Yo);
-        step(r + 1, P2, P3, Ye, Yo, Xe, Xo);
+    for (; r + kD - 1 < r1; r += kD) {
+#pragma unroll
+        for (int i = 0; i < kD; i += 2) {
+            step(r + i, P[2 * i], P[2 * i + 1], Xe, Xo, Ye, Yo);
+            step(r + i + 1, P[2 * i + 2], P[2 * i + 3], Ye, Yo, Xe, Xo);
+        }
     }
-    if (r < r1) step(r, P0, P1, Xe, Xo, Ye, Yo);
+#pragma unroll
+    for (int i = 0; i < kD; i += 2) {
+        if (r + i < r1) step(r + i, P[2 * i], P[2 * i + 1], Xe, Xo, Ye, Yo);
+        if (r + i + 1 < r1) step(r + i + 1, P[2 * i + 2], P[2 * i + 3], Ye, Yo, Xe, Xo);
+    }
 }
 
+template <int kD>
 __global__ void __launch_bounds__(64 * kL01Waves) pyr_dn_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
                                                                 int64_t src_off, int W, int H, int64_t dst_off, int W1,
                                                                 int H1, int own, int nstrip, int nband, int band_rows,
@@ -830,13 +1111,143 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_dn_kernel(uint8_t* stacks,
     const bool le = strip == 0, re = col0 + 4 * own >= W;
     const uint8_t* const src = base + src_off;
     uint8_t* const dst = base + dst_off;
-    if (le && re) dn_strip<true, true>(src, dst, W, H, W1, own, col0, r0, r1, lane);
-    else if (le) dn_strip<true, false>(src, dst, W, H, W1, own, col0, r0, r1, lane);
-    else if (re) dn_strip<false, true>(src, dst, W, H, W1, own, col0, r0, r1, lane);
-    else dn_strip<false, false>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+    if (le && re) dn_strip<true, true, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+    else if (le) dn_strip<true, false, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+    else if (re) dn_strip<false, true, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
+    else dn_strip<false, false, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
 }
 
-int pyr_mode() {  // SVO_PYR: 0 the round-4 kernels, 1 pyr_l01_kernel, 2 pyr_l01v2_kernel, 3 (default) pyr_l01v3_kernel
+// pyr_dn2_kernel: pyr_dn_kernel with pyr_l01v4's economies (buffer accesses, v_pk_mad_u16 for the 4x / 6x terms, the
+// rounding shift in the final permute, interior bands without reflection)
+template <bool kLE, bool kRE, bool kIn>
+__device__ __forceinline__ void dn2_strip(uint8_t* base, int32_t stack_bytes, uint32_t src_off, uint32_t dst_off, int W,
+                                          int H, int W1, int own, int col0, int r0, int r1, int lane) {
+    const int c0 = col0 + 4 * (lane - 1);
+    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
+    const bool owner = lane >= 1 && lane <= own;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, stack_bytes, 0x00020000);
+    const uint32_t ucl = (uint32_t)cl, ux = (uint32_t)(c0 >> 1);
+    auto prow = [&](int y) -> uint32_t {
+        return kIn ? (uint32_t)__builtin_amdgcn_readfirstlane(y) * (uint32_t)W
+                   : (uint32_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * (uint32_t)W;
+    };
+    auto raw = [&](int y) -> uint32_t {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, ucl, src_off + (prow(y) & ~3u), 0);
+    };
+    auto cook = [&](uint32_t lo, int y, uint32_t& e, uint32_t& o) {
+        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, prow(y) & 3u);
+        e = pe(v);
+        o = po(v);
+    };
+    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
+        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
+        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
+        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
+        if (kLE && c0 == 0) {
+            A = (A & 0xFFFF0000u) | (C >> 16);
+            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
+        }
+        if (kLE && kRE && W <= 2) {  // one or two columns: every tap reflects back into them (x0 only: W1 = 1)
+            const uint32_t v0 = C & 0xFFFFu, v1 = W == 2 ? (D & 0xFFFFu) : v0;
+            A = v0;
+            B = v1;
+            C = v0;
+            D = v1;
+            E = v0;
+        } else if (kRE) {
+            const int d = W - 1 - c0;
+            if (d == 0) {
+                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
+                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
+            } else if (d == 1) {
+                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
+            } else if (d == 2) {
+                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
+                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
+            } else if (d == 3) {
+                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
+            }
+        }
+        const uint32_t t = pk_mad6(C, pk_mad4(pk_add(B, D), pk_add(A, E)));
+        const uint32_t q = as_u32(as_u16x2(t) + (u16x2v){128, 128});
+        return __builtin_amdgcn_perm(0u, q, 0x0C0C0301u);
+    };
+    const bool full_1 = owner && (!kRE || (int)ux + 1 < W1), part_1 = kRE && owner && (int)ux == W1 - 1;
+    auto store = [&](int r, uint32_t v) {
+        const uint32_t so = dst_off + (uint32_t)__builtin_amdgcn_readfirstlane(r * W1);
+        if (full_1) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
+        if (kRE && part_1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, rs, ux, so, 0);
+    };
+    auto step = [&](int r, uint32_t& Pa, uint32_t& Pb, uint32_t& Xe, uint32_t& Xo, uint32_t& Ye, uint32_t& Yo) {
+        uint32_t e1, o1, e2, o2;
+        cook(Pa, 2 * r + 1, e1, o1);
+        cook(Pb, 2 * r + 2, e2, o2);
+        Pa = raw(2 * r + 5);
+        Pb = raw(2 * r + 6);
+        Xe = pk_add(pk_mad4(e1, Xe), e2);
+        Xo = pk_add(pk_mad4(o1, Xo), o2);
+        Ye = pk_mad6(e2, pk_mad4(e1, Ye));
+        Yo = pk_mad6(o2, pk_mad4(o1, Yo));
+        store(r, hpass2(Xe, Xo));
+        Xe = e2;
+        Xo = o2;
+    };
+    uint32_t Xe, Xo, Ye, Yo;
+    {
+        uint32_t e0, o0, e1, o1, e2, o2;
+        cook(raw(2 * r0 - 2), 2 * r0 - 2, e0, o0);
+        cook(raw(2 * r0 - 1), 2 * r0 - 1, e1, o1);
+        cook(raw(2 * r0), 2 * r0, e2, o2);
+        Xe = pk_mad6(e2, pk_mad4(e1, e0));
+        Xo = pk_mad6(o2, pk_mad4(o1, o0));
+        Ye = e2;
+        Yo = o2;
+    }
+    uint32_t P0 = raw(2 * r0 + 1), P1 = raw(2 * r0 + 2), P2 = raw(2 * r0 + 3), P3 = raw(2 * r0 + 4);
+    int r = r0;
+    for (; r + 1 < r1; r += 2) {
+        step(r, P0, P1, Xe, Xo, Ye, Yo);
+        step(r + 1, P2, P3, Ye, Yo, Xe, Xo);
+    }
+    if (r < r1) step(r, P0, P1, Xe, Xo, Ye, Yo);
+}
+
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_dn2_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
+                                                                 int64_t src_off, int W, int H, int64_t dst_off, int W1,
+                                                                 int H1, int own, int nstrip, int nband, int band_rows,
+                                                                 int first) {
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = blockIdx.x * kL01Waves + wv;
+    if (gw >= nstrip * nband) return;  // (wave-uniform)
+    const int strip = gw % nstrip, band = gw / nstrip;
+    uint8_t* const base = stacks + (first + (int64_t)(blockIdx.y >> 1)) * frame_stride + ((blockIdx.y & 1) ? grad_off : 0);
+    const int col0 = 4 * own * strip;
+    const int r0 = band * band_rows, r1 = min(r0 + band_rows, H1);
+    const bool le = strip == 0, re = col0 + 4 * own >= W;
+    // source rows 2 r0 - 2 .. 2 r1 + 4 (the prefetch included) inside the plane: no reflection
+    const bool in = 2 * r0 - 2 >= 0 && 2 * r1 + 4 <= H - 1;
+    const int32_t sb = (int32_t)grad_off;
+    const uint32_t so = (uint32_t)src_off, dso = (uint32_t)dst_off;
+#define SVO_DN2(LE, RE)                                                                                     \
+    if (in) dn2_strip<LE, RE, true>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);                  \
+    else dn2_strip<LE, RE, false>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);
+    if (le && re) { SVO_DN2(true, true) }
+    else if (le) { SVO_DN2(true, false) }
+    else if (re) { SVO_DN2(false, true) }
+    else { SVO_DN2(false, false) }
+#undef SVO_DN2
+}
+
+int dn_band_rows(int h) {  // SVO_DN_BAND (measurement knob, read once): output rows per band of the streaming pyrDown
+    static const int b = getenv("SVO_DN_BAND") ? atoi(getenv("SVO_DN_BAND")) : 0;
+    return b > 0 ? b : max(8, (h + 7) / 8);  // (default: bands of >= 8 rows, ~8 waves per frame-stack)
+}
+
+int pyr_mode() {  // SVO_PYR: 0 the round-4 kernels, 1 pyr_l01_kernel, 2 pyr_l01v2_kernel, 3 (default) pyr_l01v3_kernel,
+                  // 4 / 5: pyr_l01v3_kernel and the streaming pyrDown with 4 / 6 steps of rows in flight instead of 2;
+                  // 6 / 7 (timing experiments, wrong bytes): level 0/1 stores at aligned addresses / no stores;
+                  // 8: pyr_l01v3_kernel with the level-0 gradient stored as aligned dwords; 9 / 10: pyr_l01v4_kernel
+                  // with unaligned / aligned level-0 gradient stores
     static const int m = getenv("SVO_PYR") ? atoi(getenv("SVO_PYR")) : 3;  // (measurement knob, read once)
     return m;
 }
@@ -857,7 +1268,13 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
         const int own = (g.w[0] + 4 * nstrip - 1) / (4 * nstrip);
         const int nband = (g.h[1] + kL01Band - 1) / kL01Band;
         const int waves = nstrip * nband;
-        hipLaunchKernelGGL(pyr_mode() == 1 ? pyr_l01_kernel : pyr_mode() == 2 ? pyr_l01v2_kernel : pyr_l01v3_kernel,
+        hipLaunchKernelGGL(pyr_mode() == 1 ? pyr_l01_kernel : pyr_mode() == 2 ? pyr_l01v2_kernel
+                           : pyr_mode() == 4 ? pyr_l01v3_kernel<4> : pyr_mode() == 5 ? pyr_l01v3_kernel<6>
+                           : pyr_mode() == 6 ? (pyr_l01v3_kernel<2, 1>) : pyr_mode() == 7 ? (pyr_l01v3_kernel<2, 2>)
+                           : pyr_mode() == 8 ? (pyr_l01v3_kernel<2, 3>)
+                           : pyr_mode() == 9 ? pyr_l01v4_kernel<false> : pyr_mode() == 10 ? pyr_l01v4_kernel<true>
+                           : pyr_mode() == 11 ? (pyr_l01v4_kernel<false, true>)
+                                                                                       : pyr_l01v3_kernel<2>,
                            dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count), dim3(64 * kL01Waves), 0, s, stacks,
                            stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1], own, nstrip, nband, first);
         l = 2;
@@ -871,10 +1288,12 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
             const int nstrip = (w + 4 * 62 - 1) / (4 * 62);
             const int own = (w + 4 * nstrip - 1) / (4 * nstrip);
             // bands of >= 8 output rows, as many as give every frame-stack ~8 waves
-            const int band_rows = max(8, (g.h[l] + 7) / 8);
+            const int band_rows = dn_band_rows(g.h[l]);
             const int nband = (g.h[l] + band_rows - 1) / band_rows;
             const int waves = nstrip * nband;
-            hipLaunchKernelGGL(pyr_dn_kernel, dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), 2 * count),
+            hipLaunchKernelGGL(pyr_mode() == 4 ? pyr_dn_kernel<4> : pyr_mode() == 5 ? pyr_dn_kernel<6>
+                               : pyr_mode() >= 9 ? pyr_dn2_kernel : pyr_dn_kernel<2>,
+                               dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), 2 * count),
                                dim3(64 * kL01Waves), 0, s, stacks, stride, grad_off, g.off[l - 1], w, g.h[l - 1], g.off[l],
                                g.w[l], g.h[l], own, nstrip, nband, band_rows, first);
         }
