@@ -756,7 +756,8 @@ struct VSel {
         VSTAMP(8);
         const uint32_t totL = C.totL, totG = C.totG;
         uint32_t ks, lk1, rk, lk;
-        auto search = [&]() __attribute__((always_inline)) {
+        // which of L_{Ks+1}, R_{Ks}, L_{Ks} to find (bits 0, 1, 2)
+        auto search = [&](int which) __attribute__((always_inline)) {
             // the crossing: the last step whose start has G < Lc, i.e. G + L < totL (the segment's first step always)
             uint32_t pke;
             const uint32_t es = find_step(C, 2, totL, pke);
@@ -768,21 +769,23 @@ struct VSel {
             const uint32_t ra = ks + 1u, rb = totL - ks + 1u, rc = ks;
             const uint32_t G0 = pke & 0xFFFFu, L0 = pke >> 16, cg = popc(mge), cl = popc(mle);
             const uint32_t ebase = es * 64u;
-            lk1 = ra > totG ? kNone
-                  : (ra > G0 && ra <= G0 + cg) ? ebase + uni(wave_select_bit(mge, ra - G0 - 1u)) : uni(locate(C, 0, ra));
-            rk = ks == 0 ? kNone
-                 : (rb > L0 && rb <= L0 + cl) ? ebase + uni(wave_select_bit(mle, rb - L0 - 1u)) : uni(locate(C, 1, rb));
-            lk = ks == 0 ? kNone
-                 : (rc > G0 && rc <= G0 + cg) ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : uni(locate(C, 0, rc));
+            if (which & 1)
+                lk1 = ra > totG ? kNone
+                      : (ra > G0 && ra <= G0 + cg) ? ebase + uni(wave_select_bit(mge, ra - G0 - 1u)) : uni(locate(C, 0, ra));
+            if (which & 2)
+                rk = ks == 0 ? kNone
+                     : (rb > L0 && rb <= L0 + cl) ? ebase + uni(wave_select_bit(mle, rb - L0 - 1u)) : uni(locate(C, 1, rb));
+            if (which & 4)
+                lk = ks == 0 ? kNone
+                     : (rc > G0 && rc <= G0 + cg) ? ebase + uni(wave_select_bit(mge, rc - G0 - 1u)) : uni(locate(C, 0, rc));
             VSTAMP(10);
         };
-#if !defined(SVO_K2V_ALLCHAINS)
+#if defined(SVO_K2V_ONECHAIN)
         // the scalar search chain once, on wave 0 (the oldest wave, first in issue); the others wait at a barrier
         // instead of running seven more copies of it beside their SIMD partners, then read the four results
-        // (round 5, same box A/B: 165.6k -> 166.9k pairs/s alone, 168.7k -> 170.2k on top of the ILP quads;
-        // -DSVO_K2V_ALLCHAINS builds round 4's every-wave form)
+        // (round 5, same box A/B: 165.6k -> 166.9k pairs/s alone, 168.7k -> 170.2k on top of the ILP quads)
         if (wave == 0) {
-            search();
+            search(7);
             if (lane == 0) {
                 sh.srch[0] = ks;
                 sh.srch[1] = lk1;
@@ -795,8 +798,30 @@ struct VSel {
         lk1 = uni(sh.srch[1]);
         rk = uni(sh.srch[2]);
         lk = uni(sh.srch[3]);
+#elif !defined(SVO_K2V_ALLCHAINS)
+        // the three boundary searches side by side on waves 0, 1, 2 (three SIMDs), each after its own copy of the
+        // crossing search; the other waves wait at the barrier (round 5, same box: 170.1k -> 172.7k pairs/s over
+        // -DSVO_K2V_ONECHAIN, all three on wave 0; -DSVO_K2V_ALLCHAINS: round 4's every-wave form)
+        if (wave < 3) {
+            search(1 << wave);
+            if (lane == 0) {
+                if (wave == 0) {
+                    sh.srch[0] = ks;
+                    sh.srch[1] = lk1;
+                } else if (wave == 1) {
+                    sh.srch[2] = rk;
+                } else {
+                    sh.srch[3] = lk;
+                }
+            }
+        }
+        __syncthreads();
+        ks = uni(sh.srch[0]);
+        lk1 = uni(sh.srch[1]);
+        rk = uni(sh.srch[2]);
+        lk = uni(sh.srch[3]);
 #else
-        search();
+        search(7);
 #endif
         const uint32_t cut = lk1 < rk ? lk1 : rk;
         const bool right = cut <= nth;  // the side introselect continues with

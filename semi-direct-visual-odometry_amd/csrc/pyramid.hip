@@ -784,7 +784,7 @@ struct Px2 {
     uint32_t e, o;  // columns (0, 2) and (1, 3) as u16 pairs
 };
 
-template <bool kLE, bool kRE, bool kIn, bool kAl, bool kW = false>
+template <bool kLE, bool kRE, bool kIn, bool kAl, bool kW = false, int kSkip = 0, bool kPair = false>
 __device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int32_t stack_bytes, int W, int H, int64_t off1,
                                             int W1, int own, int col0, int r0, int r1, int lane) {
     const int c0 = col0 + 4 * (lane - 1);
@@ -862,10 +862,20 @@ __device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int3
     const bool full_g = owner && (!kRE || c0 + 3 < W), part_g = kRE && owner && c0 < W && c0 + 3 >= W;
     const int x = c0 >> 1;
     const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
+    // (kPair) level-1 rows: the owner lanes in pairs (1, 2), (3, 4), ...: a dword of four columns per pair; an odd
+    // last owner stores its two columns; at the right edge the pair stores its columns inside the row byte by byte
+    const bool odd = (lane & 1) == 1;
+    const bool pair_full = owner && odd && lane + 1 <= own && (!kRE || x + 3 < W1);
+    const bool pair_half = owner && odd && lane == own && (!kRE || x + 1 < W1);
+    const bool pair_part = kRE && owner && odd && !pair_full && !pair_half;
     const int ylim = min(2 * r1, H);
     auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
         if (y >= ylim) return;  // (uniform)
         const uint32_t v = ge | (go << 8);
+        if (kSkip & 1) {  // (timing experiment: no level-0 gradient stores)
+            asm volatile("" ::"v"(v));
+            return;
+        }
         const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(y * W);
         if (kAl) {
             const uint32_t sh = (uint32_t)ro & 3u;
@@ -900,6 +910,20 @@ __device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int3
     };
     auto store_l1 = [&](const __amdgpu_buffer_rsrc_t& rs, int r, uint32_t v) {
         const uint32_t so = (uint32_t)off1 + (uint32_t)__builtin_amdgcn_readfirstlane(r * W1);
+        if (kSkip & 2) {  // (timing experiment: no level-1 stores)
+            asm volatile("" ::"v"(v));
+            return;
+        }
+        if (kPair) {  // odd lane k stores one dword: its two bytes, then lane k + 1's
+            const uint32_t d = (v & 0xFFFFu) | (from_right(v) << 16);
+            if (pair_full) __builtin_amdgcn_raw_buffer_store_b32(d, rs, ux, so, 0);
+            else if (pair_half) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
+            else if (kRE && pair_part)
+                for (int i = 0; i < 4; ++i)
+                    if ((int)ux + i < W1 && (i < 2 || lane + 1 <= own))
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(d >> (8 * i)), rs, ux + (uint32_t)i, so, 0);
+            return;
+        }
         if (kW) {
             const uint32_t d = (v & 0xFFFFu) | (from_right(v) << 16);
             const uint32_t d2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0x102, 0xF, 0xF, true);
@@ -962,7 +986,7 @@ __device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int3
     if (r < r1) step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
 }
 
-template <bool kAl, bool kW = false>
+template <bool kAl, bool kW = false, int kSkip = 0, bool kPair = false>
 __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v4_kernel(uint8_t* stacks, int64_t frame_stride,
                                                                    int64_t grad_off, int W, int H, int64_t off1, int W1,
                                                                    int H1, int own, int nstrip, int nband, int first) {
@@ -980,8 +1004,8 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v4_kernel(uint8_t* stac
     const bool in = 2 * r0 - 3 >= 1 && 2 * r1 + 7 <= H - 2;
     const int32_t sb = (int32_t)grad_off;  // (each stack's bytes fit below the gradient stack's offset)
 #define SVO_L01V4(LE, RE)                                                                                   \
-    if (in) l01v4_strip<LE, RE, true, kAl, kW>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);      \
-    else l01v4_strip<LE, RE, false, kAl, kW>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);
+    if (in) l01v4_strip<LE, RE, true, kAl, kW, kSkip, kPair>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);      \
+    else l01v4_strip<LE, RE, false, kAl, kW, kSkip, kPair>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);
     if (le && re) { SVO_L01V4(true, true) }
     else if (le) { SVO_L01V4(true, false) }
     else if (re) { SVO_L01V4(false, true) }
@@ -1119,7 +1143,7 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_dn_kernel(uint8_t* stacks,
 
 // pyr_dn2_kernel: pyr_dn_kernel with pyr_l01v4's economies (buffer accesses, v_pk_mad_u16 for the 4x / 6x terms, the
 // rounding shift in the final permute, interior bands without reflection)
-template <bool kLE, bool kRE, bool kIn>
+template <bool kLE, bool kRE, bool kIn, bool kPair>
 __device__ __forceinline__ void dn2_strip(uint8_t* base, int32_t stack_bytes, uint32_t src_off, uint32_t dst_off, int W,
                                           int H, int W1, int own, int col0, int r0, int r1, int lane) {
     const int c0 = col0 + 4 * (lane - 1);
@@ -1173,8 +1197,22 @@ __device__ __forceinline__ void dn2_strip(uint8_t* base, int32_t stack_bytes, ui
         return __builtin_amdgcn_perm(0u, q, 0x0C0C0301u);
     };
     const bool full_1 = owner && (!kRE || (int)ux + 1 < W1), part_1 = kRE && owner && (int)ux == W1 - 1;
+    const bool odd = (lane & 1) == 1;  // (kPair: as pyr_l01v4's level-1 rows)
+    const bool pair_full = owner && odd && lane + 1 <= own && (!kRE || (int)ux + 3 < W1);
+    const bool pair_half = owner && odd && lane == own && (!kRE || (int)ux + 1 < W1);
+    const bool pair_part = kRE && owner && odd && !pair_full && !pair_half;
     auto store = [&](int r, uint32_t v) {
         const uint32_t so = dst_off + (uint32_t)__builtin_amdgcn_readfirstlane(r * W1);
+        if (kPair) {
+            const uint32_t d = (v & 0xFFFFu) | (from_right(v) << 16);
+            if (pair_full) __builtin_amdgcn_raw_buffer_store_b32(d, rs, ux, so, 0);
+            else if (pair_half) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
+            else if (kRE && pair_part)
+                for (int i = 0; i < 4; ++i)
+                    if ((int)ux + i < W1 && (i < 2 || lane + 1 <= own))
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(d >> (8 * i)), rs, ux + (uint32_t)i, so, 0);
+            return;
+        }
         if (full_1) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
         if (kRE && part_1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, rs, ux, so, 0);
     };
@@ -1212,6 +1250,7 @@ __device__ __forceinline__ void dn2_strip(uint8_t* base, int32_t stack_bytes, ui
     if (r < r1) step(r, P0, P1, Xe, Xo, Ye, Yo);
 }
 
+template <bool kPair>
 __global__ void __launch_bounds__(64 * kL01Waves) pyr_dn2_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
                                                                  int64_t src_off, int W, int H, int64_t dst_off, int W1,
                                                                  int H1, int own, int nstrip, int nband, int band_rows,
@@ -1229,8 +1268,8 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_dn2_kernel(uint8_t* stacks
     const int32_t sb = (int32_t)grad_off;
     const uint32_t so = (uint32_t)src_off, dso = (uint32_t)dst_off;
 #define SVO_DN2(LE, RE)                                                                                     \
-    if (in) dn2_strip<LE, RE, true>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);                  \
-    else dn2_strip<LE, RE, false>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);
+    if (in) dn2_strip<LE, RE, true, kPair>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);                  \
+    else dn2_strip<LE, RE, false, kPair>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);
     if (le && re) { SVO_DN2(true, true) }
     else if (le) { SVO_DN2(true, false) }
     else if (re) { SVO_DN2(false, true) }
@@ -1274,6 +1313,10 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
                            : pyr_mode() == 8 ? (pyr_l01v3_kernel<2, 3>)
                            : pyr_mode() == 9 ? pyr_l01v4_kernel<false> : pyr_mode() == 10 ? pyr_l01v4_kernel<true>
                            : pyr_mode() == 11 ? (pyr_l01v4_kernel<false, true>)
+                           : pyr_mode() == 12 ? (pyr_l01v4_kernel<false, false, 1>)
+                           : pyr_mode() == 13 ? (pyr_l01v4_kernel<false, false, 2>)
+                           : pyr_mode() == 14 ? (pyr_l01v4_kernel<false, false, 3>)
+                           : pyr_mode() == 15 ? (pyr_l01v4_kernel<false, false, 0, true>)
                                                                                        : pyr_l01v3_kernel<2>,
                            dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count), dim3(64 * kL01Waves), 0, s, stacks,
                            stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1], own, nstrip, nband, first);
@@ -1292,7 +1335,7 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
             const int nband = (g.h[l] + band_rows - 1) / band_rows;
             const int waves = nstrip * nband;
             hipLaunchKernelGGL(pyr_mode() == 4 ? pyr_dn_kernel<4> : pyr_mode() == 5 ? pyr_dn_kernel<6>
-                               : pyr_mode() >= 9 ? pyr_dn2_kernel : pyr_dn_kernel<2>,
+                               : pyr_mode() >= 15 ? pyr_dn2_kernel<true> : pyr_mode() >= 9 ? pyr_dn2_kernel<false> : pyr_dn_kernel<2>,
                                dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), 2 * count),
                                dim3(64 * kL01Waves), 0, s, stacks, stride, grad_off, g.off[l - 1], w, g.h[l - 1], g.off[l],
                                g.w[l], g.h[l], own, nstrip, nband, band_rows, first);
