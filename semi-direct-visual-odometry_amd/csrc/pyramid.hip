@@ -5,10 +5,13 @@
 //   level l > 0 : cv::pyrDown of level l-1 for BOTH stacks (the gradient stack is pyrDown of the
 //                 gradient, not the gradient of the downsampled image): 5x5 [1 4 6 4 1]^2 kernel,
 //                 BORDER_REFLECT_101, (sum + 128) >> 8, dst size ((w+1)/2, (h+1)/2).
-// Integer arithmetic only, so the result is bit-exact by construction.  pyrDown: each 256-thread
-// workgroup computes an 8x256 destination tile, vertical pass from global memory (a thread per source
-// column) into LDS, then the horizontal pass.  Gradient: flat
-// runs (8192 px) staged with 16-B loads, 16 pixels and one 16-B store per thread.
+// Integer arithmetic only, so the result is bit-exact by construction.  One launch per level for any number of frames
+// (DESIGN 18.4):
+//   pyr_l01_kernel   level-0 gradient + level 1 of both stacks, one register-streaming pass over the base image;
+//   pyr_dn_kernel    each later level of both stacks, register-streaming pyrDown.
+// The round-4 kernels stay behind SVO_PYR=0 for A/B measurement: abs_grad_kernel (flat 8192-px runs staged with
+// 16-B loads, 16 pixels and one 16-B store per thread) and pyr_down_kernel (8x256 destination tiles, vertical pass
+// from global memory into LDS, then the horizontal pass), one launch per level.
 #include "svo_internal.h"
 
 namespace svo {
@@ -186,16 +189,26 @@ __global__ void __launch_bounds__(kGradThreads) abs_grad_kernel(uint8_t* stacks,
 // Level-0 gradient + level 1 of BOTH stacks in one pass over the base image (pyr_l01_kernel).
 //
 // One wave streams a vertical strip of the base image down a band of level-1 rows, entirely in registers: lane l
-// holds four source columns c0 = 4 (own * strip + l - 1) .. c0 + 3 of each row as one dword (an aligned dword load
-// realigned with the right neighbour lane's dword through DPP), lanes 0 and 63 are halo lanes (their values feed
-// their neighbours' taps; they store nothing).  Per level-1 row r the wave keeps the base rows 2r-3 .. 2r+3 and
-// the gradient rows 2r-2 .. 2r+2 (Simd::AbsGradientSaturatedSum, byte-parallel; row / column neighbours by DPP);
-// the vertical [1 4 6 4 1] sums of both stacks are packed u16 pairs, the horizontal pass takes the neighbour
-// lanes' sums by DPP.  BORDER_REFLECT_101: rows through the reflected row index of each tap (every tap of a valid
-// output is one reflection away), columns by substituting the reflected sums in the edge strips.  Each output
-// row (two gradient rows of level 0, one row of each level-1 stack) leaves through the wave's 256-B LDS buffer:
-// byte writes at the row's address alignment, then aligned dword stores (the run's two partial end dwords byte by
-// byte), so every byte is written once by the wave that owns it.  Integer arithmetic only: bit-exact.
+// holds four source columns c0 = 4 (own * strip + l - 1) .. c0 + 3 of each row as one dword (an aligned dword buffer
+// load realigned with the right neighbour lane's dword through DPP), lanes 0 and 63 are halo lanes (their values
+// feed their neighbours' taps; they store nothing).  Every row is kept as two u16 pairs, columns (0, 2) and (1, 3),
+// and all arithmetic runs on packed u16 pairs (every sum of this pyramid stays below 2^16):
+//  * the gradient (Simd::AbsGradientSaturatedSum) in the pair domain: the left / right neighbours of columns (0, 2)
+//    are (-1, 1) / (1, 3) and of (1, 3) are (0, 2) / (2, 4), one DPP and one alignbyte per parity;
+//  * the vertical [1 4 6 4 1] pass as running sums: source row 2m + 1 adds 4x to level-1 rows m and m + 1, row 2m
+//    adds 1x / 6x / 1x to rows m - 1, m, m + 1, so a lane carries two partial sums per stack and the four base rows
+//    the gradient needs, and every role alternates between two register sets from one step to the next (the loop,
+//    unrolled by two, moves no register); the 4x / 6x terms are v_pk_mad_u16;
+//  * the horizontal pass takes the neighbour lanes' sums by DPP, the rounding shift folded into the final byte
+//    permute (the high bytes of sum + 128);
+//  * BORDER_REFLECT_101: rows through the reflected row index of each tap (every tap of a valid output is one
+//    reflection away; bands that touch neither the first nor the last base rows carry no reflection and no border-row
+//    test), columns by substituting the reflected sums in the edge strips.
+// The outputs leave straight from the lanes: a dword per lane per gradient row, a 16-bit pair per lane per level-1
+// row, at their (unaligned) addresses; the lanes at the right edge store byte by byte.  Integer arithmetic only:
+// bit-exact.  (Round 5 history, DESIGN 18.4: the same pass with a window of unpacked rows (v2), with the running
+// sums but per-pixel neighbour permutes (v3), with aligned-dword gradient stores or paired level-1 stores, each
+// measured slower on the same box.)
 constexpr int kL01Waves = 4;                  // independent waves per workgroup (strip x band each)
 constexpr int kL01Band = 32;                  // level-1 rows per band
 
@@ -212,564 +225,16 @@ __device__ __forceinline__ int refl101(int i, int n) {  // one reflection (valid
     return min(max(i, 0), n - 1);
 }
 
-// the lane's four pixels of plane row `row` (aligned dword + the right lane's dword); lanes outside the strip's
-// loadable range read the row start (their values are never used)
-__device__ __forceinline__ uint32_t load4(const uint8_t* plane, int W, int row, int c0) {
-    const int c = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
-    const int64_t o = (int64_t)row * W + c;
-    const uint32_t lo = *reinterpret_cast<const uint32_t*>(plane + (o & ~(int64_t)3));
-    const uint32_t hi = from_right(lo);
-    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
-}
-
-// one output row run of a wave: lanes 1..own hold K bytes each (little-endian in v) for columns
-// col0 + K (l - 1) + i; columns in [col0, ncol) go to dst_row (the plane row's column 0).  stage_run writes the
-// lane's bytes into the wave's LDS buffer at the run's address alignment; flush_run (after the stages of every run
-// of the row: one LDS round trip for all of them) stores the buffer as aligned dwords, the run's partial end dwords
-// byte by byte.
-struct Run {
-    uintptr_t A;  // address of the run's first byte
-    int n;        // bytes from the aligned dword below A to the run's end (0: empty run)
-};
-template <int K>
-__device__ __forceinline__ Run stage_run(uint8_t* dst_row, int col0, int ncol, int own, uint32_t v, uint8_t* lbuf,
-                                         int lane) {
-    const int ch = min(col0 + K * own, ncol);
-    Run r{reinterpret_cast<uintptr_t>(dst_row + col0), 0};
-    if (ch <= col0) return r;  // (wave-uniform)
-    const int sh = (int)(r.A & 3u);
-    r.n = sh + (ch - col0);
-    if (lane >= 1 && lane <= own) {
-        const int c = K * (lane - 1);
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            if (col0 + c + i < ch) lbuf[sh + c + i] = (uint8_t)(v >> (8 * i));
-    }
-    return r;
-}
-__device__ __forceinline__ void flush_run(const Run& r, const uint8_t* lbuf, int lane) {
-    const int lo = 4 * lane;
-    if (lo >= r.n) return;
-    const int sh = (int)(r.A & 3u);
-    const uint32_t w = reinterpret_cast<const uint32_t*>(lbuf)[lane];
-    uint8_t* g = reinterpret_cast<uint8_t*>(r.A & ~(uintptr_t)3) + lo;
-    if (lo >= sh && lo + 4 <= r.n) {
-        *reinterpret_cast<uint32_t*>(g) = w;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (lo + i >= sh && lo + i < r.n) g[i] = (uint8_t)(w >> (8 * i));
-    }
-}
-
 typedef uint16_t u16x2v __attribute__((ext_vector_type(2)));
-// vertical [1 4 6 4 1] sums of five rows (four pixels each): (cols 0, 2) and (cols 1, 3) as u16 pairs
-__device__ __forceinline__ void vsum5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e, uint32_t& ev,
-                                      uint32_t& od) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const u16x2v A = as_u16x2((a >> (8 * h)) & 0x00FF00FFu), B = as_u16x2((b >> (8 * h)) & 0x00FF00FFu);
-        const u16x2v C = as_u16x2((c >> (8 * h)) & 0x00FF00FFu), D = as_u16x2((d >> (8 * h)) & 0x00FF00FFu);
-        const u16x2v E = as_u16x2((e >> (8 * h)) & 0x00FF00FFu);
-        const u16x2v s = (A + E) + ((B + D) << (u16x2v){2, 2}) + C * (u16x2v){6, 6};
-        (h ? od : ev) = as_u32(s);
-    }
-}
-// the two level-1 pixels of the lane (columns c0 / 2, c0 / 2 + 1) from its vertical sums and its neighbours';
-// `edge` (wave-uniform): this strip holds column 0 or column W - 1 (reflected taps)
-__device__ __forceinline__ uint32_t hpass(uint32_t ev, uint32_t od, int c0, int W, bool edge) {
-    const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
-    uint32_t V[7] = {lev >> 16, lod >> 16, ev & 0xFFFFu, od & 0xFFFFu, ev >> 16, od >> 16, rev & 0xFFFFu};
-    if (edge) {  // columns c0 - 2 + j outside [0, W) take the sums of their BORDER_REFLECT_101 columns
-        if (c0 == 0) { V[0] = V[4]; V[1] = V[3]; }
-        const int d = W - 1 - c0;  // the lane's last valid offset from c0 (>= 4: no column past the edge)
-#pragma unroll
-        for (int j = 3; j < 7; ++j) {
-            // column c0 - 2 + j >= W  <=>  j >= d + 3; its reflection is V[2d + 4 - j]
-            uint32_t r = V[j];
-#pragma unroll
-            for (int k = 0; k < j; ++k) r = (j >= d + 3 && k == 2 * d + 4 - j) ? V[k] : r;
-            V[j] = r;
-        }
-    }
-    const uint32_t o0 = (V[0] + 4 * V[1] + 6 * V[2] + 4 * V[3] + V[4] + 128) >> 8;
-    const uint32_t o1 = (V[2] + 4 * V[3] + 6 * V[4] + 4 * V[5] + V[6] + 128) >> 8;
-    return o0 | (o1 << 8);
-}
-
-__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
-                                                                 int W, int H, int64_t off1, int W1, int H1, int own,
-                                                                 int nstrip, int nband, int first) {
-    __shared__ __attribute__((aligned(16))) uint8_t lbuf_all[kL01Waves][4][256];  // per wave: one buffer per run
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int gw = blockIdx.x * kL01Waves + wv;
-    if (gw >= nstrip * nband) return;  // (wave-uniform)
-    const int strip = gw % nstrip, band = gw / nstrip;
-    uint8_t(*const lbuf)[256] = lbuf_all[wv];
-    const int frame = first + blockIdx.y;
-    uint8_t* const ibase = stacks + frame * frame_stride;
-    uint8_t* const gbase = ibase + grad_off;
-    const int col0 = 4 * own * strip;         // the strip's first owned source column
-    const int c0 = col0 + 4 * (lane - 1);     // this lane's
-    const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
-    const bool edge = strip == 0 || col0 + 4 * own >= W;
-    // border columns of the gradient (Simd leaves them 0): byte masks of this lane
-    uint32_t colmask = 0xFFFFFFFFu;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (c0 + i == 0 || c0 + i == W - 1) colmask &= ~(0xFFu << (8 * i));
-    auto row_of = [&](int y) { return refl101(y, H); };
-    auto ld = [&](int y) { return load4(ibase, W, row_of(y), c0); };
-    auto grad = [&](uint32_t up, uint32_t mid, uint32_t dn, int y) -> uint32_t {
-        const uint32_t L = from_left(mid), R = from_right(mid);
-        const uint32_t g = grad4(__builtin_amdgcn_alignbyte(mid, L, 3), __builtin_amdgcn_alignbyte(R, mid, 1), up, dn);
-        const int py = row_of(y);
-        return (py == 0 || py == H - 1) ? 0u : (g & colmask);
-    };
-    // window: R[k] = base row (logical) 2r - 3 + k, G[i] = gradient row 2r - 2 + i; P: the base rows of the next
-    // two iterations, in flight
-    uint32_t R[7], G[5], P[4];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) R[k] = ld(2 * r0 - 3 + k);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) P[k] = ld(2 * r0 + 4 + k);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) G[i] = grad(R[i], R[i + 1], R[i + 2], 2 * r0 - 2 + i);
-    for (int r = r0; r < r1; ++r) {
-        // level 1 of both stacks
-        uint32_t ev, od;
-        vsum5(R[1], R[2], R[3], R[4], R[5], ev, od);
-        const uint32_t oi = hpass(ev, od, c0, W, edge);
-        vsum5(G[0], G[1], G[2], G[3], G[4], ev, od);
-        const uint32_t og = hpass(ev, od, c0, W, edge);
-        // the row's four runs: level-0 gradient rows 2r, 2r + 1 (this band's own source rows), level-1 rows
-        const Run q0 = stage_run<4>(gbase + (int64_t)(2 * r) * W, col0, W, own, G[2], lbuf[0], lane);
-        const Run q1 = 2 * r + 1 < H ? stage_run<4>(gbase + (int64_t)(2 * r + 1) * W, col0, W, own, G[3], lbuf[1], lane)
-                                     : Run{0, 0};
-        const Run q2 = stage_run<2>(ibase + off1 + (int64_t)r * W1, col0 / 2, W1, own, oi, lbuf[2], lane);
-        const Run q3 = stage_run<2>(gbase + off1 + (int64_t)r * W1, col0 / 2, W1, own, og, lbuf[3], lane);
-        asm volatile("" ::: "memory");  // (the dword reads take other lanes' bytes: LDS keeps a wave's order)
-        flush_run(q0, lbuf[0], lane);
-        flush_run(q1, lbuf[1], lane);
-        flush_run(q2, lbuf[2], lane);
-        flush_run(q3, lbuf[3], lane);
-        asm volatile("" ::: "memory");  // (the next row rewrites the buffers)
-        // advance the window by two base rows
-#pragma unroll
-        for (int k = 0; k < 5; ++k) R[k] = R[k + 2];
-        R[5] = P[0];
-        R[6] = P[1];
-        P[0] = P[2];
-        P[1] = P[3];
-        P[2] = ld(2 * r + 8);
-        P[3] = ld(2 * r + 9);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) G[i] = G[i + 2];
-        G[3] = grad(R[3], R[4], R[5], 2 * r + 3);
-        G[4] = grad(R[4], R[5], R[6], 2 * r + 4);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// pyr_l01v2_kernel: the same pass with every row kept unpacked as well (u16 pairs of columns (0, 2) and (1, 3)), the
-// gradient, the vertical sums and the horizontal pass all on packed u16 pairs (the horizontal [1 4 6 4 1] sum of
-// level-1 sums stays below 2^16), the row addresses on scalars (the rows' alignment is uniform: every lane's c0 is
-// a multiple of 4), and the outputs stored straight from the lanes: a dword per lane per gradient row and a 16-bit
-// pair per lane per level-1 row, at their (unaligned) addresses; the lanes at the right edge store byte by byte.
-struct Px4 {
-    uint32_t p, e, o;  // four pixels; columns (0, 2) and (1, 3) as u16 pairs
-};
 __device__ __forceinline__ uint32_t pe(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C020C00u); }  // b0, b2
 __device__ __forceinline__ uint32_t po(uint32_t v) { return __builtin_amdgcn_perm(0u, v, 0x0C030C01u); }  // b1, b3
 __device__ __forceinline__ uint32_t pk_absdiff(uint32_t a, uint32_t b) {
     return as_u32(__builtin_elementwise_max(as_u16x2(a), as_u16x2(b)) - __builtin_elementwise_min(as_u16x2(a), as_u16x2(b)));
 }
 __device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return as_u32(as_u16x2(a) + as_u16x2(b)); }
-// [1 4 6 4 1] over five u16 pairs (every sum of this pyramid stays below 2^16)
-__device__ __forceinline__ uint32_t pk_tap5(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
-    const u16x2v s = (as_u16x2(a) + as_u16x2(e)) + ((as_u16x2(b) + as_u16x2(d)) << (u16x2v){2, 2}) +
-                     as_u16x2(c) * (u16x2v){6, 6};
-    return as_u32(s);
-}
-
-// one strip x band of pyr_l01v2_kernel; kLE / kRE: the strip holds column 0 / column W - 1 (reflected taps, the
-// partial last lanes), so the interior strips carry none of that code
-template <bool kLE, bool kRE>
-__device__ __forceinline__ void l01v2_strip(uint8_t* ibase, uint8_t* gbase, int W, int H, int64_t off1, int W1, int own,
-                                            int col0, int r0, int r1, int lane) {
-    const int c0 = col0 + 4 * (lane - 1);
-    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;  // the lane's load column (never used when clamped)
-    const bool owner = lane >= 1 && lane <= own;
-    // the gradient's border columns (Simd leaves them 0) as u16-pair masks
-    uint32_t me = 0xFFFFFFFFu, mo = 0xFFFFFFFFu;
-    if (kLE && c0 == 0) me &= 0xFFFF0000u;
-    if (kRE) {
-        if (c0 == W - 1) me &= 0xFFFF0000u;
-        if (c0 + 2 == W - 1) me &= 0x0000FFFFu;
-        if (c0 + 1 == W - 1) mo &= 0xFFFF0000u;
-        if (c0 + 3 == W - 1) mo &= 0x0000FFFFu;
-    }
-    const uint8_t* const lbase = ibase + cl;
-    // (uniform) the aligned offset of row refl101(y) and its byte shift: every lane's c0 is 0 mod 4
-    auto rowoff = [&](int y, uint32_t& sh) -> int64_t {
-        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
-        sh = (uint32_t)(ro & 3);
-        return ro & ~(int64_t)3;
-    };
-    auto raw = [&](int y) -> uint32_t {
-        uint32_t sh;
-        return *reinterpret_cast<const uint32_t*>(lbase + rowoff(y, sh));
-    };
-    auto cook = [&](uint32_t lo, int y) -> Px4 {
-        uint32_t sh;
-        (void)rowoff(y, sh);
-        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, sh);
-        return Px4{v, pe(v), po(v)};
-    };
-    auto grad = [&](const Px4& up, const Px4& mid, const Px4& dn, int y, uint32_t& ge, uint32_t& go) {
-        const uint32_t L = from_left(mid.p), R = from_right(mid.p);
-        const uint32_t l = __builtin_amdgcn_alignbyte(mid.p, L, 3), r = __builtin_amdgcn_alignbyte(R, mid.p, 1);
-        const u16x2v lim = {255, 255};
-        ge = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(pe(l), pe(r)), pk_absdiff(up.e, dn.e))), lim));
-        go = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(po(l), po(r)), pk_absdiff(up.o, dn.o))), lim));
-        const int py = __builtin_amdgcn_readfirstlane(refl101(y, H));
-        if (py == 0 || py == H - 1) {  // (uniform)
-            ge = 0u;
-            go = 0u;
-        }
-        if (kLE || kRE) {
-            ge &= me;
-            go &= mo;
-        }
-    };
-    // the two level-1 pixels of the lane from the vertical sums ev (columns 0, 2), od (1, 3): packed pairs
-    // A = (c-2, c0), B = (c-1, c1), C = (c0, c2), D = (c1, c3), E = (c2, c4) -> (x0, x1) = A + 4B + 6C + 4D + E
-    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
-        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
-        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
-        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
-        if (kLE && c0 == 0) {  // columns -2, -1 -> 2, 1 (BORDER_REFLECT_101)
-            A = (A & 0xFFFF0000u) | (C >> 16);
-            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
-        }
-        if (kRE) {  // columns >= W -> 2W - 2 - c, for the outputs this lane stores
-            const int d = W - 1 - c0;
-            if (d == 0) {  // x0 only: c1 <- c-1, c2 <- c-2
-                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
-                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
-            } else if (d == 1) {  // x0 only: c2 <- c0
-                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
-            } else if (d == 2) {  // x1: c3 <- c1, c4 <- c0
-                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
-                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
-            } else if (d == 3) {  // x1: c4 <- c2
-                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
-            }
-        }
-        const u16x2v t = as_u16x2(pk_tap5(A, B, C, D, E)) + (u16x2v){128, 128};
-        const uint32_t q = as_u32(t >> (u16x2v){8, 8});
-        return __builtin_amdgcn_perm(0u, q, 0x0C0C0200u);  // x0 | x1 << 8
-    };
-    // stores: a dword (gradient row) / a 16-bit pair (level-1 row) per owner lane at its own address; the lanes
-    // holding the row's last column write their part byte by byte
-    const bool full_g = owner && (!kRE || c0 + 3 < W), part_g = kRE && owner && c0 < W && c0 + 3 >= W;
-    const int x = c0 >> 1;
-    const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
-    auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
-        const uint32_t v = ge | (go << 8);
-        uint8_t* const d = gbase + (int64_t)__builtin_amdgcn_readfirstlane(y * W) + c0;
-        if (full_g) *reinterpret_cast<uint32_t*>(d) = v;
-        if (kRE && part_g)
-            for (int i = 0; i < 4; ++i)
-                if (c0 + i < W) d[i] = (uint8_t)(v >> (8 * i));
-    };
-    auto store_l1 = [&](uint8_t* plane, int r, uint32_t v) {
-        uint8_t* const d = plane + off1 + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
-        if (full_1) *reinterpret_cast<uint16_t*>(d) = (uint16_t)v;
-        if (kRE && part_1) d[0] = (uint8_t)v;
-    };
-    Px4 R[7];
-    uint32_t GE[5], GO[5];
-    uint32_t P[4];  // raw aligned dwords of the next two iterations' rows (in flight)
-#pragma unroll
-    for (int k = 0; k < 7; ++k) R[k] = cook(raw(2 * r0 - 3 + k), 2 * r0 - 3 + k);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) grad(R[i], R[i + 1], R[i + 2], 2 * r0 - 2 + i, GE[i], GO[i]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) P[k] = raw(2 * r0 + 4 + k);
-#pragma unroll 2
-    for (int r = r0; r < r1; ++r) {
-        store_grad(2 * r, GE[2], GO[2]);
-        if (2 * r + 1 < H) store_grad(2 * r + 1, GE[3], GO[3]);
-        const uint32_t ei = pk_tap5(R[1].e, R[2].e, R[3].e, R[4].e, R[5].e);
-        const uint32_t oi = pk_tap5(R[1].o, R[2].o, R[3].o, R[4].o, R[5].o);
-        store_l1(ibase, r, hpass2(ei, oi));
-        const uint32_t eg = pk_tap5(GE[0], GE[1], GE[2], GE[3], GE[4]);
-        const uint32_t og = pk_tap5(GO[0], GO[1], GO[2], GO[3], GO[4]);
-        store_l1(gbase, r, hpass2(eg, og));
-#pragma unroll
-        for (int k = 0; k < 5; ++k) R[k] = R[k + 2];
-        R[5] = cook(P[0], 2 * r + 4);
-        R[6] = cook(P[1], 2 * r + 5);
-        P[0] = P[2];
-        P[1] = P[3];
-        P[2] = raw(2 * r + 8);
-        P[3] = raw(2 * r + 9);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            GE[i] = GE[i + 2];
-            GO[i] = GO[i + 2];
-        }
-        grad(R[3], R[4], R[5], 2 * r + 3, GE[3], GO[3]);
-        grad(R[4], R[5], R[6], 2 * r + 4, GE[4], GO[4]);
-    }
-}
-
-__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v2_kernel(uint8_t* stacks, int64_t frame_stride,
-                                                                   int64_t grad_off, int W, int H, int64_t off1, int W1,
-                                                                   int H1, int own, int nstrip, int nband, int first) {
-    // (the wave index through readfirstlane: everything derived from it is uniform and lives in SGPRs)
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gw = blockIdx.x * kL01Waves + wv;
-    if (gw >= nstrip * nband) return;  // (wave-uniform)
-    const int strip = gw % nstrip, band = gw / nstrip;
-    uint8_t* const ibase = stacks + (first + (int64_t)blockIdx.y) * frame_stride;
-    uint8_t* const gbase = ibase + grad_off;
-    const int col0 = 4 * own * strip;
-    const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
-    const bool le = strip == 0, re = col0 + 4 * own >= W;
-    if (le && re) l01v2_strip<true, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else if (le) l01v2_strip<true, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else if (re) l01v2_strip<false, true>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else l01v2_strip<false, false>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// pyr_l01v3_kernel: pyr_l01v2's arithmetic with the vertical [1 4 6 4 1] pass as running sums instead of a window of
-// rows: source row 2m + 1 adds 4x to level-1 rows m and m + 1, row 2m adds 1x / 6x / 1x to rows m - 1, m, m + 1, so
-// a lane carries two partial sums per stack and the four base rows the gradient needs, and every role alternates
-// between two register sets from one step to the next: the loop, unrolled by two, moves no register.
 struct Acc {
     uint32_t ie, io, ge, go;  // intensity / gradient partial sums, columns (0, 2) and (1, 3)
 };
-__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t k, uint32_t c) {  // a * k + c on u16 pairs
-    return as_u32(as_u16x2(a) * (u16x2v){(uint16_t)k, (uint16_t)k} + as_u16x2(c));
-}
-
-template <bool kLE, bool kRE, int kD, int kX = 0>
-__device__ __forceinline__ void l01v3_strip(uint8_t* ibase, uint8_t* gbase, int W, int H, int64_t off1, int W1, int own,
-                                            int col0, int r0, int r1, int lane) {
-    const int c0 = col0 + 4 * (lane - 1);
-    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;  // the lane's load column (never used when clamped)
-    const bool owner = lane >= 1 && lane <= own;
-    uint32_t me = 0xFFFFFFFFu, mo = 0xFFFFFFFFu;  // the gradient's border columns as u16-pair masks
-    if (kLE && c0 == 0) me &= 0xFFFF0000u;
-    if (kRE) {
-        if (c0 == W - 1) me &= 0xFFFF0000u;
-        if (c0 + 2 == W - 1) me &= 0x0000FFFFu;
-        if (c0 + 1 == W - 1) mo &= 0xFFFF0000u;
-        if (c0 + 3 == W - 1) mo &= 0x0000FFFFu;
-    }
-    const uint8_t* const lbase = ibase + cl;
-    auto rowoff = [&](int y, uint32_t& sh) -> int64_t {
-        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
-        sh = (uint32_t)(ro & 3);
-        return ro & ~(int64_t)3;
-    };
-    auto raw = [&](int y) -> uint32_t {
-        uint32_t sh;
-        return *reinterpret_cast<const uint32_t*>(lbase + rowoff(y, sh));
-    };
-    auto cook = [&](uint32_t lo, int y) -> Px4 {
-        uint32_t sh;
-        (void)rowoff(y, sh);
-        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, sh);
-        return Px4{v, pe(v), po(v)};
-    };
-    auto grad = [&](const Px4& up, const Px4& mid, const Px4& dn, int y, uint32_t& ge, uint32_t& go) {
-        const uint32_t L = from_left(mid.p), R = from_right(mid.p);
-        const uint32_t l = __builtin_amdgcn_alignbyte(mid.p, L, 3), r = __builtin_amdgcn_alignbyte(R, mid.p, 1);
-        const u16x2v lim = {255, 255};
-        ge = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(pe(l), pe(r)), pk_absdiff(up.e, dn.e))), lim));
-        go = as_u32(__builtin_elementwise_min(as_u16x2(pk_add(pk_absdiff(po(l), po(r)), pk_absdiff(up.o, dn.o))), lim));
-        const int py = __builtin_amdgcn_readfirstlane(refl101(y, H));
-        if (py == 0 || py == H - 1) {  // (uniform)
-            ge = 0u;
-            go = 0u;
-        }
-        if (kLE || kRE) {
-            ge &= me;
-            go &= mo;
-        }
-    };
-    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
-        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
-        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
-        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
-        if (kLE && c0 == 0) {  // columns -2, -1 -> 2, 1 (BORDER_REFLECT_101)
-            A = (A & 0xFFFF0000u) | (C >> 16);
-            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
-        }
-        if (kRE) {  // columns >= W -> 2W - 2 - c, for the outputs this lane stores
-            const int d = W - 1 - c0;
-            if (d == 0) {
-                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
-                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
-            } else if (d == 1) {
-                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
-            } else if (d == 2) {
-                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
-                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
-            } else if (d == 3) {
-                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
-            }
-        }
-        const u16x2v t = as_u16x2(pk_tap5(A, B, C, D, E)) + (u16x2v){128, 128};
-        const uint32_t q = as_u32(t >> (u16x2v){8, 8});
-        return __builtin_amdgcn_perm(0u, q, 0x0C0C0200u);  // x0 | x1 << 8
-    };
-    const bool full_g = owner && (!kRE || c0 + 3 < W), part_g = kRE && owner && c0 < W && c0 + 3 >= W;
-    const int x = c0 >> 1;
-    const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
-    const int ylim = min(2 * r1, H);  // this band's own base rows: [2 r0, ylim)
-    auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
-        if (y >= ylim) return;  // (uniform)
-        const uint32_t v = ge | (go << 8);
-        if (kX == 3) {  // aligned dwords: the lane stores columns c0 - s .. c0 - s + 3 (s: the row's misalignment)
-            const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(y * W);
-            const uint32_t sh = (uint32_t)ro & 3u;
-            const uint32_t w = __builtin_amdgcn_perm(v, from_left(v), 0x07060504u - sh * 0x01010101u);
-            uint8_t* const da = gbase + (ro - (int64_t)sh) + c0;
-            const int lo = c0 - (int)sh;  // the dword's first column
-            if (!kLE && !kRE) {
-                if (owner) *reinterpret_cast<uint32_t*>(da) = w;
-            } else {
-                // (edge strips: the strip's first dword starts before column 0, the last one runs past W - 1: those
-                // lanes store their row's bytes one by one; the lane after the last owner carries its tail)
-                const bool any = lane >= 1 && lo <= W - 1 && lane <= (kRE ? own + 1 : own);
-                if (any && lo >= 0 && lo + 3 <= W - 1) *reinterpret_cast<uint32_t*>(da) = w;
-                else if (any)
-                    for (int i = 0; i < 4; ++i)
-                        if (lo + i >= 0 && lo + i <= W - 1) da[i] = (uint8_t)(w >> (8 * i));
-            }
-            return;
-        }
-        uint8_t* d = gbase + (int64_t)__builtin_amdgcn_readfirstlane(y * W) + c0;
-        if (kX == 1) d = (uint8_t*)((uintptr_t)d & ~(uintptr_t)3);  // (timing experiment only: wrong bytes)
-        if (kX == 2) return;
-        if (full_g) *reinterpret_cast<uint32_t*>(d) = v;
-        if (kRE && part_g)
-            for (int i = 0; i < 4; ++i)
-                if (c0 + i < W) d[i] = (uint8_t)(v >> (8 * i));
-    };
-    auto store_l1 = [&](uint8_t* plane, int r, uint32_t v) {
-        uint8_t* d = plane + off1 + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
-        if (kX == 1) d = (uint8_t*)((uintptr_t)d & ~(uintptr_t)1);
-        if (kX == 2) {  // (keep the value live)
-            asm volatile("" ::"v"(v));
-            return;
-        }
-        if (full_1) *reinterpret_cast<uint16_t*>(d) = (uint16_t)v;
-        if (kRE && part_1) d[0] = (uint8_t)v;
-    };
-    // one level-1 row r: holds I(2r), I(2r + 1) in I0, I1, takes the raw rows 2r + 2, 2r + 3 from Pa, Pb (reloads
-    // them with the rows kD steps ahead, 2r + 2 + 2kD and 2r + 3 + 2kD), leaves I(2r + 2), I(2r + 3) in I2, I3; X: the sums of row r (completed and stored
-    // here, then restarted as row r + 2's), Y: row r + 1's
-    auto step = [&](int r, const Px4& I0, const Px4& I1, Px4& I2, Px4& I3, uint32_t& Pa, uint32_t& Pb, Acc& X, Acc& Y) {
-        I2 = cook(Pa, 2 * r + 2);
-        I3 = cook(Pb, 2 * r + 3);
-        Pa = raw(2 * r + 2 + 2 * kD);
-        Pb = raw(2 * r + 3 + 2 * kD);
-        uint32_t g1e, g1o, g2e, g2o;
-        grad(I0, I1, I2, 2 * r + 1, g1e, g1o);
-        grad(I1, I2, I3, 2 * r + 2, g2e, g2o);
-        store_grad(2 * r + 1, g1e, g1o);
-        store_grad(2 * r + 2, g2e, g2o);
-        if (kX == 2) asm volatile("" ::"v"(g1e), "v"(g1o), "v"(g2e), "v"(g2o));
-        // row 2r + 1: 4x into rows r and r + 1; row 2r + 2: 1x into r (complete), 6x into r + 1, 1x starts r + 2
-        X.ie = pk_add(pk_mad(I1.e, 4, X.ie), I2.e);
-        X.io = pk_add(pk_mad(I1.o, 4, X.io), I2.o);
-        X.ge = pk_add(pk_mad(g1e, 4, X.ge), g2e);
-        X.go = pk_add(pk_mad(g1o, 4, X.go), g2o);
-        Y.ie = pk_mad(I2.e, 6, pk_mad(I1.e, 4, Y.ie));
-        Y.io = pk_mad(I2.o, 6, pk_mad(I1.o, 4, Y.io));
-        Y.ge = pk_mad(g2e, 6, pk_mad(g1e, 4, Y.ge));
-        Y.go = pk_mad(g2o, 6, pk_mad(g1o, 4, Y.go));
-        store_l1(ibase, r, hpass2(X.ie, X.io));
-        store_l1(gbase, r, hpass2(X.ge, X.go));
-        X = Acc{I2.e, I2.o, g2e, g2o};
-    };
-    // the state at r0: I(2r0 - 3 .. 2r0 + 1), gradients 2r0 - 2 .. 2r0, row r0's sums over 2r0 - 2 .. 2r0, row
-    // r0 + 1's over 2r0
-    Px4 Ia, Ib, Ic, Id;
-    Acc X, Y;
-    {
-        const Px4 Jm3 = cook(raw(2 * r0 - 3), 2 * r0 - 3), Jm2 = cook(raw(2 * r0 - 2), 2 * r0 - 2);
-        const Px4 Jm1 = cook(raw(2 * r0 - 1), 2 * r0 - 1);
-        Ia = cook(raw(2 * r0), 2 * r0);
-        Ib = cook(raw(2 * r0 + 1), 2 * r0 + 1);
-        uint32_t hm2e, hm2o, hm1e, hm1o, h0e, h0o;
-        grad(Jm3, Jm2, Jm1, 2 * r0 - 2, hm2e, hm2o);
-        grad(Jm2, Jm1, Ia, 2 * r0 - 1, hm1e, hm1o);
-        grad(Jm1, Ia, Ib, 2 * r0, h0e, h0o);
-        store_grad(2 * r0, h0e, h0o);
-        X.ie = pk_mad(Ia.e, 6, pk_mad(Jm1.e, 4, Jm2.e));
-        X.io = pk_mad(Ia.o, 6, pk_mad(Jm1.o, 4, Jm2.o));
-        X.ge = pk_mad(h0e, 6, pk_mad(hm1e, 4, hm2e));
-        X.go = pk_mad(h0o, 6, pk_mad(hm1o, 4, hm2o));
-        Y = Acc{Ia.e, Ia.o, h0e, h0o};
-    }
-    // kD steps of raw rows in flight; the loop unrolled by kD (even) so that every role keeps its registers
-    static_assert(kD % 2 == 0, "the running sums alternate between two register sets");
-    uint32_t P[2 * kD];
-#pragma unroll
-    for (int k = 0; k < 2 * kD; ++k) P[k] = raw(2 * r0 + 2 + k);
-    int r = r0;
-    for (; r + kD - 1 < r1; r += kD) {
-#pragma unroll
-        for (int i = 0; i < kD; i += 2) {
-            step(r + i, Ia, Ib, Ic, Id, P[2 * i], P[2 * i + 1], X, Y);
-            step(r + i + 1, Ic, Id, Ia, Ib, P[2 * i + 2], P[2 * i + 3], Y, X);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < kD; i += 2) {  // the band's last r1 - r < kD rows (uniform)
-        if (r + i < r1) step(r + i, Ia, Ib, Ic, Id, P[2 * i], P[2 * i + 1], X, Y);
-        if (r + i + 1 < r1) step(r + i + 1, Ic, Id, Ia, Ib, P[2 * i + 2], P[2 * i + 3], Y, X);
-    }
-}
-
-template <int kD, int kX = 0>
-__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v3_kernel(uint8_t* stacks, int64_t frame_stride,
-                                                                   int64_t grad_off, int W, int H, int64_t off1, int W1,
-                                                                   int H1, int own, int nstrip, int nband, int first) {
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gw = blockIdx.x * kL01Waves + wv;
-    if (gw >= nstrip * nband) return;  // (wave-uniform)
-    const int strip = gw % nstrip, band = gw / nstrip;
-    uint8_t* const ibase = stacks + (first + (int64_t)blockIdx.y) * frame_stride;
-    uint8_t* const gbase = ibase + grad_off;
-    const int col0 = 4 * own * strip;
-    const int r0 = band * kL01Band, r1 = min(r0 + kL01Band, H1);
-    const bool le = strip == 0, re = col0 + 4 * own >= W;
-    if (le && re) l01v3_strip<true, true, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else if (le) l01v3_strip<true, false, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else if (re) l01v3_strip<false, true, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-    else l01v3_strip<false, false, kD, kX>(ibase, gbase, W, H, off1, W1, own, col0, r0, r1, lane);
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// pyr_l01v4_kernel: pyr_l01v3's pass with fewer VALU per step (the profile of v3: VALU ~2/3 busy, the texture
-// addresser ~3/4 busy):
-//  * the horizontal gradient in the pair domain: the left / right neighbours of columns (0, 2) are (-1, 1) / (1, 3)
-//    and of (1, 3) are (0, 2) / (2, 4): one DPP and one alignbyte per parity instead of two DPPs, two alignbytes
-//    and four byte permutes on the unpacked row;
-//  * the running sums' 4x terms as v_pk_mad_u16 (the compiler's choice was a shift and an add);
-//  * the rounding shift of the horizontal pass folded into the final byte permute (the high bytes of sum + 128);
-//  * bands that touch neither the first nor the last base rows (kIn) carry no row reflection and no border-row test;
-//  * (kAl) the level-0 gradient leaves as aligned dwords: the lane stores columns c0 - s .. c0 - s + 3 of its row (s the
-//    row's misalignment), the bytes of the left lane's last s columns by one DPP and one permute; the lanes whose
-//    dword leaves the row store bytes.
 __device__ __forceinline__ uint32_t pk_mad4(uint32_t a, uint32_t c) {  // a * 4 + c on u16 pairs, one instruction
     uint32_t r;
     asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(c));
@@ -784,8 +249,8 @@ struct Px2 {
     uint32_t e, o;  // columns (0, 2) and (1, 3) as u16 pairs
 };
 
-template <bool kLE, bool kRE, bool kIn, bool kAl, bool kW = false, int kSkip = 0, bool kPair = false>
-__device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int32_t stack_bytes, int W, int H, int64_t off1,
+template <bool kLE, bool kRE, bool kIn>
+__device__ __forceinline__ void l01_strip(uint8_t* ibase, uint8_t* gbase, int32_t stack_bytes, int W, int H, int64_t off1,
                                             int W1, int own, int col0, int r0, int r1, int lane) {
     const int c0 = col0 + 4 * (lane - 1);
     const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
@@ -862,47 +327,11 @@ __device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int3
     const bool full_g = owner && (!kRE || c0 + 3 < W), part_g = kRE && owner && c0 < W && c0 + 3 >= W;
     const int x = c0 >> 1;
     const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
-    // (kPair) level-1 rows: the owner lanes in pairs (1, 2), (3, 4), ...: a dword of four columns per pair; an odd
-    // last owner stores its two columns; at the right edge the pair stores its columns inside the row byte by byte
-    const bool odd = (lane & 1) == 1;
-    const bool pair_full = owner && odd && lane + 1 <= own && (!kRE || x + 3 < W1);
-    const bool pair_half = owner && odd && lane == own && (!kRE || x + 1 < W1);
-    const bool pair_part = kRE && owner && odd && !pair_full && !pair_half;
     const int ylim = min(2 * r1, H);
     auto store_grad = [&](int y, uint32_t ge, uint32_t go) {
         if (y >= ylim) return;  // (uniform)
         const uint32_t v = ge | (go << 8);
-        if (kSkip & 1) {  // (timing experiment: no level-0 gradient stores)
-            asm volatile("" ::"v"(v));
-            return;
-        }
         const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(y * W);
-        if (kAl) {
-            const uint32_t sh = (uint32_t)ro & 3u;
-            const uint32_t w = __builtin_amdgcn_perm(v, from_left(v), 0x07060504u - sh * 0x01010101u);
-            const uint32_t so = (uint32_t)(ro - (int64_t)sh);
-            const int lo = c0 - (int)sh;  // the dword's first column
-            if (!kLE && !kRE) {
-                if (owner) __builtin_amdgcn_raw_buffer_store_b32(w, rg, uc0, so, 0);
-            } else {
-                const bool any = lane >= 1 && lo <= W - 1 && lane <= (kRE ? own + 1 : own);
-                if (any && lo >= 0 && lo + 3 <= W - 1) __builtin_amdgcn_raw_buffer_store_b32(w, rg, uc0, so, 0);
-                else if (any)
-                    for (int i = 0; i < 4; ++i)
-                        if (lo + i >= 0 && lo + i <= W - 1)
-                            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> (8 * i)), rg, uc0 + (uint32_t)i, so, 0);
-            }
-            return;
-        }
-        if (kW) {  // (timing experiment: 16-B stores from every fourth lane, the quad's dwords by DPP; strip-edge bytes wrong)
-            const uint32_t g1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xF, 0xF, true);
-            const uint32_t g2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x102, 0xF, 0xF, true);
-            const uint32_t g3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x103, 0xF, 0xF, true);
-            typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-            if (owner && (lane & 3) == 0 && c0 + 15 < W)
-                __builtin_amdgcn_raw_buffer_store_b128((u32x4v){v, g1, g2, g3}, rg, uc0, (uint32_t)ro, 0);
-            return;
-        }
         if (full_g) __builtin_amdgcn_raw_buffer_store_b32(v, rg, uc0, (uint32_t)ro, 0);
         if (kRE && part_g)
             for (int i = 0; i < 4; ++i)
@@ -910,30 +339,6 @@ __device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int3
     };
     auto store_l1 = [&](const __amdgpu_buffer_rsrc_t& rs, int r, uint32_t v) {
         const uint32_t so = (uint32_t)off1 + (uint32_t)__builtin_amdgcn_readfirstlane(r * W1);
-        if (kSkip & 2) {  // (timing experiment: no level-1 stores)
-            asm volatile("" ::"v"(v));
-            return;
-        }
-        if (kPair) {  // odd lane k stores one dword: its two bytes, then lane k + 1's
-            const uint32_t d = (v & 0xFFFFu) | (from_right(v) << 16);
-            if (pair_full) __builtin_amdgcn_raw_buffer_store_b32(d, rs, ux, so, 0);
-            else if (pair_half) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
-            else if (kRE && pair_part)
-                for (int i = 0; i < 4; ++i)
-                    if ((int)ux + i < W1 && (i < 2 || lane + 1 <= own))
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(d >> (8 * i)), rs, ux + (uint32_t)i, so, 0);
-            return;
-        }
-        if (kW) {
-            const uint32_t d = (v & 0xFFFFu) | (from_right(v) << 16);
-            const uint32_t d2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0x102, 0xF, 0xF, true);
-            const uint32_t d4 = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0x104, 0xF, 0xF, true);
-            const uint32_t d6 = (uint32_t)__builtin_amdgcn_mov_dpp((int)d, 0x106, 0xF, 0xF, true);
-            typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
-            if (owner && (lane & 7) == 0 && (int)ux + 15 < W1)
-                __builtin_amdgcn_raw_buffer_store_b128((u32x4v){d, d2, d4, d6}, rs, ux, so, 0);
-            return;
-        }
         if (full_1) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
         if (kRE && part_1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, rs, ux, so, 0);
     };
@@ -986,8 +391,7 @@ __device__ __forceinline__ void l01v4_strip(uint8_t* ibase, uint8_t* gbase, int3
     if (r < r1) step(r, Ia, Ib, Ic, Id, P0, P1, X, Y);
 }
 
-template <bool kAl, bool kW = false, int kSkip = 0, bool kPair = false>
-__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v4_kernel(uint8_t* stacks, int64_t frame_stride,
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_l01_kernel(uint8_t* stacks, int64_t frame_stride,
                                                                    int64_t grad_off, int W, int H, int64_t off1, int W1,
                                                                    int H1, int own, int nstrip, int nband, int first) {
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1003,148 +407,24 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_l01v4_kernel(uint8_t* stac
     // inside [1, H - 2]: no reflection, no border row
     const bool in = 2 * r0 - 3 >= 1 && 2 * r1 + 7 <= H - 2;
     const int32_t sb = (int32_t)grad_off;  // (each stack's bytes fit below the gradient stack's offset)
-#define SVO_L01V4(LE, RE)                                                                                   \
-    if (in) l01v4_strip<LE, RE, true, kAl, kW, kSkip, kPair>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);      \
-    else l01v4_strip<LE, RE, false, kAl, kW, kSkip, kPair>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);
-    if (le && re) { SVO_L01V4(true, true) }
-    else if (le) { SVO_L01V4(true, false) }
-    else if (re) { SVO_L01V4(false, true) }
-    else { SVO_L01V4(false, false) }
-#undef SVO_L01V4
+#define SVO_L01(LE, RE)                                                                                     \
+    if (in) l01_strip<LE, RE, true>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);               \
+    else l01_strip<LE, RE, false>(ibase, gbase, sb, W, H, off1, W1, own, col0, r0, r1, lane);
+    if (le && re) { SVO_L01(true, true) }
+    else if (le) { SVO_L01(true, false) }
+    else if (re) { SVO_L01(false, true) }
+    else { SVO_L01(false, false) }
+#undef SVO_L01
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// pyr_dn_kernel: cv::pyrDown of one level of either stack (levels >= 2), the register-streaming form of
-// pyr_l01v3_kernel without the gradient: lane l takes four source columns, two running sums per lane, two output
-// pixels per lane and output row, unrolled by two so that no register moves.  grid.y = 2 * frames (stack, frame).
-template <bool kLE, bool kRE, int kD>
-__device__ __forceinline__ void dn_strip(const uint8_t* src, uint8_t* dst, int W, int H, int W1, int own, int col0,
-                                         int r0, int r1, int lane) {
-    const int c0 = col0 + 4 * (lane - 1);
-    const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
-    const bool owner = lane >= 1 && lane <= own;
-    const uint8_t* const lbase = src + cl;
-    auto raw = [&](int y) -> uint32_t {
-        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
-        return *reinterpret_cast<const uint32_t*>(lbase + (ro & ~(int64_t)3));
-    };
-    auto cook = [&](uint32_t lo, int y, uint32_t& e, uint32_t& o) {
-        const int64_t ro = (int64_t)__builtin_amdgcn_readfirstlane(refl101(y, H)) * W;
-        const uint32_t v = __builtin_amdgcn_alignbyte(from_right(lo), lo, (uint32_t)(ro & 3));
-        e = pe(v);
-        o = po(v);
-    };
-    auto hpass2 = [&](uint32_t ev, uint32_t od) -> uint32_t {
-        const uint32_t lev = from_left(ev), lod = from_left(od), rev = from_right(ev);
-        uint32_t A = __builtin_amdgcn_alignbyte(ev, lev, 2), B = __builtin_amdgcn_alignbyte(od, lod, 2);
-        uint32_t C = ev, D = od, E = __builtin_amdgcn_alignbyte(rev, ev, 2);
-        if (kLE && c0 == 0) {
-            A = (A & 0xFFFF0000u) | (C >> 16);
-            B = (B & 0xFFFF0000u) | (D & 0xFFFFu);
-        }
-        if (kLE && kRE && W <= 2) {  // one or two columns: every tap reflects back into them (x0 only: W1 = 1)
-            const uint32_t v0 = C & 0xFFFFu, v1 = W == 2 ? (D & 0xFFFFu) : v0;
-            A = v0;
-            B = v1;
-            C = v0;
-            D = v1;
-            E = v0;
-        } else if (kRE) {
-            const int d = W - 1 - c0;
-            if (d == 0) {
-                D = (D & 0xFFFF0000u) | (B & 0xFFFFu);
-                E = (E & 0xFFFF0000u) | (A & 0xFFFFu);
-            } else if (d == 1) {
-                E = (E & 0xFFFF0000u) | (C & 0xFFFFu);
-            } else if (d == 2) {
-                D = (D & 0xFFFFu) | (B & 0xFFFF0000u);
-                E = (E & 0xFFFFu) | (A & 0xFFFF0000u);
-            } else if (d == 3) {
-                E = (E & 0xFFFFu) | (C & 0xFFFF0000u);
-            }
-        }
-        const u16x2v t = as_u16x2(pk_tap5(A, B, C, D, E)) + (u16x2v){128, 128};
-        const uint32_t q = as_u32(t >> (u16x2v){8, 8});
-        return __builtin_amdgcn_perm(0u, q, 0x0C0C0200u);
-    };
-    const int x = c0 >> 1;
-    const bool full_1 = owner && (!kRE || x + 1 < W1), part_1 = kRE && owner && x == W1 - 1;
-    auto store = [&](int r, uint32_t v) {
-        uint8_t* const d = dst + (int64_t)__builtin_amdgcn_readfirstlane(r * W1) + x;
-        if (full_1) *reinterpret_cast<uint16_t*>(d) = (uint16_t)v;
-        if (kRE && part_1) d[0] = (uint8_t)v;
-    };
-    // row r: takes the raw rows 2r + 1, 2r + 2 from Pa, Pb (reloads them with 2r + 5, 2r + 6); X the sums of row r
-    // (stored, then restarted as row r + 2's), Y row r + 1's
-    auto step = [&](int r, uint32_t& Pa, uint32_t& Pb, uint32_t& Xe, uint32_t& Xo, uint32_t& Ye, uint32_t& Yo) {
-        uint32_t e1, o1, e2, o2;
-        cook(Pa, 2 * r + 1, e1, o1);
-        cook(Pb, 2 * r + 2, e2, o2);
-        Pa = raw(2 * r + 1 + 2 * kD);
-        Pb = raw(2 * r + 2 + 2 * kD);
-        Xe = pk_add(pk_mad(e1, 4, Xe), e2);
-        Xo = pk_add(pk_mad(o1, 4, Xo), o2);
-        Ye = pk_mad(e2, 6, pk_mad(e1, 4, Ye));
-        Yo = pk_mad(o2, 6, pk_mad(o1, 4, Yo));
-        store(r, hpass2(Xe, Xo));
-        Xe = e2;
-        Xo = o2;
-    };
-    uint32_t Xe, Xo, Ye, Yo;
-    {
-        uint32_t e0, o0, e1, o1, e2, o2;
-        cook(raw(2 * r0 - 2), 2 * r0 - 2, e0, o0);
-        cook(raw(2 * r0 - 1), 2 * r0 - 1, e1, o1);
-        cook(raw(2 * r0), 2 * r0, e2, o2);
-        Xe = pk_mad(e2, 6, pk_mad(e1, 4, e0));
-        Xo = pk_mad(o2, 6, pk_mad(o1, 4, o0));
-        Ye = e2;
-        Yo = o2;
-    }
-    static_assert(kD % 2 == 0, "the running sums alternate between two register sets");
-    uint32_t P[2 * kD];
-#pragma unroll
-    for (int k = 0; k < 2 * kD; ++k) P[k] = raw(2 * r0 + 1 + k);
-    int r = r0;
-    for (; r + kD - 1 < r1; r += kD) {
-#pragma unroll
-        for (int i = 0; i < kD; i += 2) {
-            step(r + i, P[2 * i], P[2 * i + 1], Xe, Xo, Ye, Yo);
-            step(r + i + 1, P[2 * i + 2], P[2 * i + 3], Ye, Yo, Xe, Xo);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < kD; i += 2) {
-        if (r + i < r1) step(r + i, P[2 * i], P[2 * i + 1], Xe, Xo, Ye, Yo);
-        if (r + i + 1 < r1) step(r + i + 1, P[2 * i + 2], P[2 * i + 3], Ye, Yo, Xe, Xo);
-    }
-}
-
-template <int kD>
-__global__ void __launch_bounds__(64 * kL01Waves) pyr_dn_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
-                                                                int64_t src_off, int W, int H, int64_t dst_off, int W1,
-                                                                int H1, int own, int nstrip, int nband, int band_rows,
-                                                                int first) {
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gw = blockIdx.x * kL01Waves + wv;
-    if (gw >= nstrip * nband) return;  // (wave-uniform)
-    const int strip = gw % nstrip, band = gw / nstrip;
-    uint8_t* const base = stacks + (first + (int64_t)(blockIdx.y >> 1)) * frame_stride + ((blockIdx.y & 1) ? grad_off : 0);
-    const int col0 = 4 * own * strip;
-    const int r0 = band * band_rows, r1 = min(r0 + band_rows, H1);
-    const bool le = strip == 0, re = col0 + 4 * own >= W;
-    const uint8_t* const src = base + src_off;
-    uint8_t* const dst = base + dst_off;
-    if (le && re) dn_strip<true, true, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
-    else if (le) dn_strip<true, false, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
-    else if (re) dn_strip<false, true, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
-    else dn_strip<false, false, kD>(src, dst, W, H, W1, own, col0, r0, r1, lane);
-}
-
-// pyr_dn2_kernel: pyr_dn_kernel with pyr_l01v4's economies (buffer accesses, v_pk_mad_u16 for the 4x / 6x terms, the
-// rounding shift in the final permute, interior bands without reflection)
-template <bool kLE, bool kRE, bool kIn, bool kPair>
-__device__ __forceinline__ void dn2_strip(uint8_t* base, int32_t stack_bytes, uint32_t src_off, uint32_t dst_off, int W,
+// pyr_dn_kernel: cv::pyrDown of one level of either stack (levels >= 2),
+// the register-streaming form of pyr_l01_kernel without the gradient: lane l takes four source columns as two u16
+// pairs, two running sums per lane, two output pixels per lane and output row, unrolled by two so that no register
+// moves; buffer accesses, v_pk_mad_u16 for the 4x / 6x terms, the rounding shift in the final permute, interior bands
+// without reflection.  grid.y = 2 * frames (stack, frame).
+template <bool kLE, bool kRE, bool kIn>
+__device__ __forceinline__ void dn_strip(uint8_t* base, int32_t stack_bytes, uint32_t src_off, uint32_t dst_off, int W,
                                           int H, int W1, int own, int col0, int r0, int r1, int lane) {
     const int c0 = col0 + 4 * (lane - 1);
     const int cl = (c0 >= 0 && c0 <= W + 3) ? c0 : 0;
@@ -1197,22 +477,8 @@ __device__ __forceinline__ void dn2_strip(uint8_t* base, int32_t stack_bytes, ui
         return __builtin_amdgcn_perm(0u, q, 0x0C0C0301u);
     };
     const bool full_1 = owner && (!kRE || (int)ux + 1 < W1), part_1 = kRE && owner && (int)ux == W1 - 1;
-    const bool odd = (lane & 1) == 1;  // (kPair: as pyr_l01v4's level-1 rows)
-    const bool pair_full = owner && odd && lane + 1 <= own && (!kRE || (int)ux + 3 < W1);
-    const bool pair_half = owner && odd && lane == own && (!kRE || (int)ux + 1 < W1);
-    const bool pair_part = kRE && owner && odd && !pair_full && !pair_half;
     auto store = [&](int r, uint32_t v) {
         const uint32_t so = dst_off + (uint32_t)__builtin_amdgcn_readfirstlane(r * W1);
-        if (kPair) {
-            const uint32_t d = (v & 0xFFFFu) | (from_right(v) << 16);
-            if (pair_full) __builtin_amdgcn_raw_buffer_store_b32(d, rs, ux, so, 0);
-            else if (pair_half) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
-            else if (kRE && pair_part)
-                for (int i = 0; i < 4; ++i)
-                    if ((int)ux + i < W1 && (i < 2 || lane + 1 <= own))
-                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(d >> (8 * i)), rs, ux + (uint32_t)i, so, 0);
-            return;
-        }
         if (full_1) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, rs, ux, so, 0);
         if (kRE && part_1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, rs, ux, so, 0);
     };
@@ -1250,8 +516,7 @@ __device__ __forceinline__ void dn2_strip(uint8_t* base, int32_t stack_bytes, ui
     if (r < r1) step(r, P0, P1, Xe, Xo, Ye, Yo);
 }
 
-template <bool kPair>
-__global__ void __launch_bounds__(64 * kL01Waves) pyr_dn2_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
+__global__ void __launch_bounds__(64 * kL01Waves) pyr_dn_kernel(uint8_t* stacks, int64_t frame_stride, int64_t grad_off,
                                                                  int64_t src_off, int W, int H, int64_t dst_off, int W1,
                                                                  int H1, int own, int nstrip, int nband, int band_rows,
                                                                  int first) {
@@ -1267,30 +532,20 @@ __global__ void __launch_bounds__(64 * kL01Waves) pyr_dn2_kernel(uint8_t* stacks
     const bool in = 2 * r0 - 2 >= 0 && 2 * r1 + 4 <= H - 1;
     const int32_t sb = (int32_t)grad_off;
     const uint32_t so = (uint32_t)src_off, dso = (uint32_t)dst_off;
-#define SVO_DN2(LE, RE)                                                                                     \
-    if (in) dn2_strip<LE, RE, true, kPair>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);                  \
-    else dn2_strip<LE, RE, false, kPair>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);
-    if (le && re) { SVO_DN2(true, true) }
-    else if (le) { SVO_DN2(true, false) }
-    else if (re) { SVO_DN2(false, true) }
-    else { SVO_DN2(false, false) }
-#undef SVO_DN2
+#define SVO_DN(LE, RE)                                                                                      \
+    if (in) dn_strip<LE, RE, true>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);                      \
+    else dn_strip<LE, RE, false>(base, sb, so, dso, W, H, W1, own, col0, r0, r1, lane);
+    if (le && re) { SVO_DN(true, true) }
+    else if (le) { SVO_DN(true, false) }
+    else if (re) { SVO_DN(false, true) }
+    else { SVO_DN(false, false) }
+#undef SVO_DN
 }
-
-int dn_band_rows(int h) {  // SVO_DN_BAND (measurement knob, read once): output rows per band of the streaming pyrDown
-    static const int b = getenv("SVO_DN_BAND") ? atoi(getenv("SVO_DN_BAND")) : 0;
-    return b > 0 ? b : max(8, (h + 7) / 8);  // (default: bands of >= 8 rows, ~8 waves per frame-stack)
-}
-
-int pyr_mode() {  // SVO_PYR: 0 the round-4 kernels, 1 pyr_l01_kernel, 2 pyr_l01v2_kernel, 3 (default) pyr_l01v3_kernel,
-                  // 4 / 5: pyr_l01v3_kernel and the streaming pyrDown with 4 / 6 steps of rows in flight instead of 2;
-                  // 6 / 7 (timing experiments, wrong bytes): level 0/1 stores at aligned addresses / no stores;
-                  // 8: pyr_l01v3_kernel with the level-0 gradient stored as aligned dwords; 9 / 10: pyr_l01v4_kernel
-                  // with unaligned / aligned level-0 gradient stores
-    static const int m = getenv("SVO_PYR") ? atoi(getenv("SVO_PYR")) : 3;  // (measurement knob, read once)
+int pyr_mode() {  // SVO_PYR (measurement knob, read once): 0 the round-4 kernels (abs_grad_kernel, pyr_down_kernel per
+                  // level), 1 (default) pyr_l01_kernel + pyr_dn_kernel per level
+    static const int m = getenv("SVO_PYR") ? atoi(getenv("SVO_PYR")) : 1;
     return m;
 }
-
 
 }  // namespace
 
@@ -1307,39 +562,23 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
         const int own = (g.w[0] + 4 * nstrip - 1) / (4 * nstrip);
         const int nband = (g.h[1] + kL01Band - 1) / kL01Band;
         const int waves = nstrip * nband;
-        hipLaunchKernelGGL(pyr_mode() == 1 ? pyr_l01_kernel : pyr_mode() == 2 ? pyr_l01v2_kernel
-                           : pyr_mode() == 4 ? pyr_l01v3_kernel<4> : pyr_mode() == 5 ? pyr_l01v3_kernel<6>
-                           : pyr_mode() == 6 ? (pyr_l01v3_kernel<2, 1>) : pyr_mode() == 7 ? (pyr_l01v3_kernel<2, 2>)
-                           : pyr_mode() == 8 ? (pyr_l01v3_kernel<2, 3>)
-                           : pyr_mode() == 9 ? pyr_l01v4_kernel<false> : pyr_mode() == 10 ? pyr_l01v4_kernel<true>
-                           : pyr_mode() == 11 ? (pyr_l01v4_kernel<false, true>)
-                           : pyr_mode() == 12 ? (pyr_l01v4_kernel<false, false, 1>)
-                           : pyr_mode() == 13 ? (pyr_l01v4_kernel<false, false, 2>)
-                           : pyr_mode() == 14 ? (pyr_l01v4_kernel<false, false, 3>)
-                           : pyr_mode() == 15 ? (pyr_l01v4_kernel<false, false, 0, true>)
-                                                                                       : pyr_l01v3_kernel<2>,
-                           dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count), dim3(64 * kL01Waves), 0, s, stacks,
-                           stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1], own, nstrip, nband, first);
+        hipLaunchKernelGGL(pyr_l01_kernel, dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), count), dim3(64 * kL01Waves),
+                           0, s, stacks, stride, grad_off, g.w[0], g.h[0], g.off[1], g.w[1], g.h[1], own, nstrip, nband, first);
         l = 2;
+        for (; l < g.levels; ++l) {
+            const int w = g.w[l - 1];
+            const int ns = (w + 4 * 62 - 1) / (4 * 62);
+            const int ow = (w + 4 * ns - 1) / (4 * ns);
+            const int band_rows = max(8, (g.h[l] + 7) / 8);  // bands of >= 8 output rows, ~8 waves per frame-stack
+            const int nb = (g.h[l] + band_rows - 1) / band_rows;
+            const int wv = ns * nb;
+            hipLaunchKernelGGL(pyr_dn_kernel, dim3((unsigned)((wv + kL01Waves - 1) / kL01Waves), 2 * count),
+                               dim3(64 * kL01Waves), 0, s, stacks, stride, grad_off, g.off[l - 1], w, g.h[l - 1], g.off[l],
+                               g.w[l], g.h[l], ow, ns, nb, band_rows, first);
+        }
     } else {
         hipLaunchKernelGGL(abs_grad_kernel, dim3((unsigned)((npx + kGradRun - 1) / kGradRun), count), dim3(kGradThreads), 0,
                            s, stacks, stride, grad_off, g.w[0], g.h[0], first);
-    }
-    if (pyr_mode() >= 3) {  // levels >= 2: the streaming pyrDown, both stacks in one launch per level
-        for (; l < g.levels; ++l) {
-            const int w = g.w[l - 1];
-            const int nstrip = (w + 4 * 62 - 1) / (4 * 62);
-            const int own = (w + 4 * nstrip - 1) / (4 * nstrip);
-            // bands of >= 8 output rows, as many as give every frame-stack ~8 waves
-            const int band_rows = dn_band_rows(g.h[l]);
-            const int nband = (g.h[l] + band_rows - 1) / band_rows;
-            const int waves = nstrip * nband;
-            hipLaunchKernelGGL(pyr_mode() == 4 ? pyr_dn_kernel<4> : pyr_mode() == 5 ? pyr_dn_kernel<6>
-                               : pyr_mode() >= 15 ? pyr_dn2_kernel<true> : pyr_mode() >= 9 ? pyr_dn2_kernel<false> : pyr_dn_kernel<2>,
-                               dim3((unsigned)((waves + kL01Waves - 1) / kL01Waves), 2 * count),
-                               dim3(64 * kL01Waves), 0, s, stacks, stride, grad_off, g.off[l - 1], w, g.h[l - 1], g.off[l],
-                               g.w[l], g.h[l], own, nstrip, nband, band_rows, first);
-        }
     }
     for (; l < g.levels; ++l) {
         dim3 grid((g.w[l] + kDnW - 1) / kDnW, (g.h[l] + kDnH - 1) / kDnH, 2 * count);
