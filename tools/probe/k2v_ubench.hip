@@ -1,7 +1,7 @@
 // k2v_ubench.hip — cycle costs of K2V's per-row primitives on gfx950 (diagnostic, not part of the product).
-// One workgroup of 64 / 128 / 256 / 512 threads (1, 2, 4, 8 waves: 2 waves share a SIMD from 8 on) runs each
+// One workgroup of 64 / 256 / 512 / 1024 threads (1, 4, 8, 16 waves: 2 waves share a SIMD from 8 on, 4 at 16) runs each
 // variant's loop of kIters x 4 rows on register-resident doubles; thread 0 of every wave reports clock64 cycles per
-// row.  Variants: the classification quad (round-4 serial form through VCC / the compares-first form), the
+// row, and the workgroup's aggregate rows per 1000 cycles (waves x rows / the slowest wave's cycles).  Variants: the classification quad (round-4 serial form through VCC / the compares-first form), the
 // compares alone, the exchange-source quad (round-4 serial form / independent per-row chains), a v_readlane ->
 // SALU -> v_readlane ping-pong, an LDS write -> read round trip.
 //   hipcc -O3 --offload-arch=gfx950 -o tools/probe_bin/k2v_ubench tools/probe/k2v_ubench.hip
@@ -16,7 +16,7 @@ __device__ int ub_writelane(int v, int l, int old) __asm("llvm.amdgcn.writelane.
 __device__ __forceinline__ uint32_t wl(uint32_t old, uint32_t v, int l) { return (uint32_t)ub_writelane((int)v, l, (int)old); }
 
 template <int V>
-__global__ void __launch_bounds__(512) ubench(double* io, uint64_t* cyc, uint32_t* sink) {
+__global__ void __launch_bounds__(1024) ubench(double* io, uint64_t* cyc, uint32_t* sink) {
     __shared__ double mb[4096];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     double x0 = io[tid], x1 = io[tid + 512], x2 = io[tid + 1024], x3 = io[tid + 1536];
@@ -134,8 +134,8 @@ int main() {
     uint64_t* cyc;
     uint32_t* sink;
     (void)hipMalloc(&io, 8 * 5000);
-    (void)hipMalloc(&cyc, 8 * 8);
-    (void)hipMalloc(&sink, 4 * 512);
+    (void)hipMalloc(&cyc, 8 * 16);
+    (void)hipMalloc(&sink, 4 * 1024);
     double h[5000];
     for (int i = 0; i < 5000; ++i) h[i] = (i * 37 % 101) - 50.0;
     h[4096] = 0.5;
@@ -146,14 +146,17 @@ int main() {
     void (*ks[])(double*, uint64_t*, uint32_t*) = {ubench<0>, ubench<1>, ubench<2>, ubench<3>, ubench<4>, ubench<5>,
                                                    ubench<6>};
     for (int v = 0; v < 7; ++v) {
-        for (int nw : {1, 4, 8}) {
+        for (int nw : {1, 4, 8, 16}) {
             hipLaunchKernelGGL(ks[v], dim3(1), dim3(64 * nw), 0, 0, io, cyc, sink);  // warm
             hipLaunchKernelGGL(ks[v], dim3(1), dim3(64 * nw), 0, 0, io, cyc, sink);
-            uint64_t c[8] = {};
+            uint64_t c[16] = {};
             (void)hipMemcpy(c, cyc, 8 * nw, hipMemcpyDeviceToHost);
-            const double per = v >= 5 ? 4.0 : 4.0;  // (per row: 4 rows per iteration; V5: 4 ping-pongs; V6: 1 trip)
-            printf("%-42s waves %d: cycles per row  w0 %.1f  w%d %.1f\n", names[v], nw, c[0] / (double)kIters / (v == 6 ? 1.0 : per),
-                   nw - 1, c[nw - 1] / (double)kIters / (v == 6 ? 1.0 : per));
+            const double per = v == 6 ? 1.0 : 4.0;  // (rows per iteration: 4; V5: 4 ping-pongs; V6: 1 round trip)
+            uint64_t cmax = 0;
+            for (int w = 0; w < nw; ++w) cmax = c[w] > cmax ? c[w] : cmax;
+            printf("%-42s waves %2d: cycles per row  w0 %.1f  w%d %.1f   aggregate rows per 1000 cycles %.1f\n", names[v], nw,
+                   c[0] / (double)kIters / per, nw - 1, c[nw - 1] / (double)kIters / per,
+                   1000.0 * nw * kIters * per / (double)cmax);
         }
     }
     hipError_t e = hipDeviceSynchronize();
