@@ -229,7 +229,7 @@ def main():
         elapsed = float(t.item())
 
     poses, err, status = batch.results()
-    # every pair repeats its scene's pose bit for bit (pairs i and i + 256 run in different half-batch chains)
+    # every pair repeats its scene's pose bit for bit (the pairs of one scene run in different sub-batch chains)
     poses_repeat = bool(all(np.array_equal(poses[i], poses[rep[sidx[i]]]) and err[i] == err[rep[sidx[i]]]
                             for i in range(P)))
     if args.dump_poses:  # every rank's per-pair results, gathered in rank order (host side, outside the timing)
@@ -304,7 +304,7 @@ def main():
         del ps2
     # the other median semantics on the same pairs: its rate and how far its poses are from the reference's
     other = svo_amd.MEDIAN_EXACT if mode == svo_amd.MEDIAN_REFERENCE else svo_amd.MEDIAN_REFERENCE
-    other_line, lat = None, None
+    other_line, lat, scaling_lines = None, None, None
     if not args.core_only:
         b2 = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx, median_mode=other)
         b2.set_pairs(0, ps, ps, ps, *packed)
@@ -323,6 +323,7 @@ def main():
                       "max_abs_pose_param_diff_vs_headline": dpose,
                       "note": "same pairs; exact order statistics are not the reference's numbers (DESIGN.md)"}
         lat = latency_lines(ctx, scenes, camera, cam, patch, L, nf, mode)
+        scaling_lines = batch_scaling(args, ctx, scenes, sidx, camera, cam, patch, L, nf, D, mode, poses)
     if rank != 0:
         if dist:
             dist.barrier()
@@ -353,7 +354,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": f"align chain: {L} levels x (K1 residual [+ pair init at the first level], K2 robust scale, "
-                               f"K3 weights + LM step), {3 * L} launches per chain, 2 concurrent half-batch chains",
+                               f"K3 weights + LM step), {3 * L} launches per chain, {n_chains(P, mode)} concurrent "
+                               f"sub-batch chains",
                      "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": b_pair * P,
                      "algorithmic_bytes_per_pair": b_pair, "traffic_source": traffic_src,
                      "stages_ms": {k: round(v, 4) for k, v in stages.items()},
@@ -395,6 +397,7 @@ def main():
             "note": "the same hand-over for a stream of batches: batch i+1's pyramids build "
                     "(svo_pyramid_set_build_async, a second PyramidSet) while batch i aligns"},
         "latency": lat,
+        "batch_scaling": scaling_lines,
     }
     if not args.no_secondary:
         out["secondary"] = secondary(args, ctx, scenes[0], cam, camera)
@@ -404,6 +407,48 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def n_chains(P, mode):
+    """Concurrent sub-batch chains run_batch uses (csrc/capi.hip: kSplitMin, kSplits, kSplitsRefv*; the bench's vectors
+    always fit K2V)."""
+    if P < 64:
+        return 1
+    return 4 if mode == svo_amd.MEDIAN_REFERENCE and P >= 512 else 2
+
+
+def batch_scaling(args, ctx, scenes, sidx, camera, cam, patch, L, nf, D, mode, poses):
+    """The same workload at 2x and 4x the pairs per GPU (each pair with its own three pyramids, uploaded and built
+    like the headline's), steps timed like the headline; every pair's pose must equal the headline's pair of the same
+    scene bit for bit.  Not `value`: the headline's batch stays the round-to-round workload."""
+    P = len(sidx)
+    out = {}
+    for mult in (2, 4):
+        Q = mult * P
+        idx = sidx * mult
+        ps = svo_amd.PyramidSet(3 * Q, cam["width"], cam["height"], L, ctx)
+        for c, arr in image_chunks(scenes, idx, D):
+            ps.upload(3 * c, arr)
+        ps.build()
+        b = svo_amd.AlignBatch(camera, patch, 0, L - 1, Q, nf, ctx, median_mode=mode)
+        b.set_pairs(0, ps, ps, ps, *packed_pairs(scenes, Q, D, idx))
+        for _ in range(2):
+            b.run()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            b.run()
+        ctx.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        pq, _, _ = b.results()
+        same = bool(all(np.array_equal(pq[j], poses[j % P]) for j in range(Q)))
+        b.close()
+        ps.close()
+        out[f"pairs_per_gpu_{Q}"] = {"pairs_per_s": round(Q / dt, 1), "ms_per_step": round(dt * 1e3, 4),
+                                     "chains": n_chains(Q, mode), "poses_equal_headline": same}
+    out["note"] = ("the headline's workload with more pairs per GPU per step (more independent chains fill the CUs a "
+                   "K2V launch frees); not the headline value")
+    return out
 
 
 def latency_lines(ctx, scenes, camera, cam, patch, L, nf, mode, reps=20):

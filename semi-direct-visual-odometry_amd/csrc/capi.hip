@@ -56,6 +56,11 @@ svo::LevelGeom make_geom(int32_t w, int32_t h, int32_t levels) {
 
 constexpr int32_t kSplitMin = 64;  // batches of at least this many pairs run as kSplits concurrent chains
 constexpr int kSplits = 2;         // measured on MI355X at 512 pairs: 1 / 2 / 3 / 4 chains = 335k / 355k / 359k / 352k pairs/s
+// reference mode on K2V (one pair per CU for the whole robust scale): more chains give the other chains' K1 / K3 more
+// ways into the CUs a K2V launch frees pair by pair (MI355X, round 5, same box: 512 pairs 2 / 4 chains = 172.4-172.9k /
+// 173.7-174.0k pairs/s; 1024 pairs 174.4-175.0k / 177.9-178.0k; 3 chains at 512: 169.6-170.2k)
+constexpr int kSplitsRefv = 4;
+constexpr int32_t kSplitsRefvMin = 512;
 
 struct svo_ctx {
     int32_t device;
@@ -835,7 +840,10 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         // independent of the split.
         static const int env_chains = getenv("SVO_CHAINS") ? atoi(getenv("SVO_CHAINS")) : 0;  // (measurement knobs,
         static const int env_stagger = getenv("SVO_STAGGER") ? atoi(getenv("SVO_STAGGER")) : -1;  //  read once)
-        const int ns = env_chains ? std::max(2, std::min(4, env_chains)) : kSplits;
+        const bool k2v = svo::scale_impl() != SVO_SCALE_K2R && (int64_t)a.max_slots <= svo::refv_max_slots();
+        const bool refv = b->params.median_mode == SVO_MEDIAN_REFERENCE && k2v;
+        const int ns = env_chains ? std::max(2, std::min(4, env_chains))
+                                  : (refv && b->n_pairs >= kSplitsRefvMin ? kSplitsRefv : kSplits);
         const int32_t per = (b->n_pairs / ns + 7) / 8 * 8;
         // Reference semantics with K2R: chain 1 starts when chain 0's first K1 is done (launch mark 2), so that
         // each chain's K1 / K3 run under the other chain's K2R instead of both chains meeting in K1 / K3 at every
@@ -844,7 +852,6 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
         // K2V (the default reference-mode kernel whenever the vector fits its registers) fills whole CUs, so
         // the other chain's K1 / K3 run only between its launches whatever the stagger: unstaggered measured
         // best (MI355X, 512 pairs: stagger 0 / 1 / 2 / 3 = 119.1k / 118.4k / 117.3k / 117.4k pairs/s).
-        const bool k2v = svo::scale_impl() != SVO_SCALE_K2R && (int64_t)a.max_slots <= svo::refv_max_slots();
         const int stagger = env_stagger >= 0 ? env_stagger
                                              : (b->params.median_mode == SVO_MEDIAN_REFERENCE && !k2v ? 2 : 0);
         if (stagger < 0 || stagger > 1 + 3 * (b->params.max_level - b->params.min_level + 1))

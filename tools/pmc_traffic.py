@@ -4,7 +4,7 @@ Correction per MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports half the 
 so it is doubled; WRITE_SIZE is taken as is.  Both are KiB per dispatch.  Traffic of one chain launch
 (= one bench step over all pairs) = sum over the chain's kernels of the per-dispatch bytes, divided by
 the number of bench steps in the profiled process: dispatches of align_scale_kernel (K2, once per level
-and chain) / (levels x --chains); a batch of >= 64 pairs runs as two concurrent half-batch chains.
+and chain) / (levels x --chains); the bench's 512-pair reference-mode batch runs as four concurrent chains.
 
 usage: python3 tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> --pairs P --features N --levels L
        --patch S > profiles/pmc_traffic.json
@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--features", type=int, default=2000)
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--patch", type=int, default=5)
-    ap.add_argument("--chains", type=int, default=2, help="concurrent chains per bench step")
+    ap.add_argument("--chains", type=int, default=4, help="concurrent chains per bench step (bench.py n_chains)")
     a = ap.parse_args()
     fetch, runs_f = per_kernel(a.fetch_dir, "FETCH_SIZE")
     write, runs_w = per_kernel(a.write_dir, "WRITE_SIZE")
