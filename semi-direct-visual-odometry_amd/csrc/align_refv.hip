@@ -183,7 +183,10 @@ struct VSel {
     static constexpr uint32_t kMbCap = L::kMbCap;
     static constexpr int kQuads = (R + 3) / 4;  // quads of rows the block rounds walk (kGenQuads of them in registers)
     // below this many rows a wave classifies and exchanges row by row (indexed registers) instead of walking the quads
-    static constexpr int kFewRows = 8;
+#ifndef SVO_FEWROWS
+#define SVO_FEWROWS 8
+#endif
+    static constexpr int kFewRows = SVO_FEWROWS;
 #ifndef SVO_QG
 #define SVO_QG 4
 #endif
