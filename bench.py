@@ -280,7 +280,7 @@ def main():
     # context's prep stream (a second PyramidSet) while batch i's features are handed over and it aligns
     # (src/frame.cpp:26 builds each frame's pyramid before the frame is aligned); per batch: one build, one
     # set_pairs, one alignment, one read-back
-    e2p_ms = None
+    e2p_ms = e2q_ms = None
     if not args.core_only:
         ps2 = svo_amd.PyramidSet(3 * P, cam["width"], cam["height"], L, ctx)
         for c, arr in chunks:
@@ -300,6 +300,28 @@ def main():
                 raise SystemExit("bench.py: pipelined end-to-end poses differ from the timed run")
         e2p_ms = (time.perf_counter() - e2p_t0) / K * 1e3
         ctx.synchronize()
+        # two batches in flight: batch i + 1's features go up (copy stream) and its pyramids build (prep stream) while
+        # batch i aligns; then batch i's results come back and batch i + 1 is queued
+        batch2 = svo_amd.AlignBatch(camera, patch, 0, L - 1, P, nf, ctx, median_mode=mode)
+        bats = (batch, batch2)
+        ps.build()
+        bats[0].set_pairs(0, ps, ps, ps, *packed)
+        ctx.synchronize()
+        e2q_t0 = time.perf_counter()
+        bats[0].run()
+        for i in range(K):
+            cur_b, nxt_b = bats[i % 2], bats[(i + 1) % 2]
+            nxt_s = sets[(i + 1) % 2]
+            if i + 1 < K:
+                nxt_s.build_async()
+                nxt_b.set_pairs(0, nxt_s, nxt_s, nxt_s, *packed)
+            pk, _, _ = cur_b.results()
+            if not np.array_equal(pk, poses):
+                raise SystemExit("bench.py: two-batch end-to-end poses differ from the timed run")
+            if i + 1 < K:
+                nxt_b.run()
+        e2q_ms = (time.perf_counter() - e2q_t0) / K * 1e3
+        batch2.close()
         batch.set_pairs(0, ps, ps, ps, *packed)  # (back on the first set)
         del ps2
     # the other median semantics on the same pairs: its rate and how far its poses are from the reference's
@@ -396,6 +418,11 @@ def main():
             "statistic": "mean over a stream of 8 batches",
             "note": "the same hand-over for a stream of batches: batch i+1's pyramids build "
                     "(svo_pyramid_set_build_async, a second PyramidSet) while batch i aligns"},
+        "end_to_end_device_images_two_batches": None if e2q_ms is None else {
+            "pairs": P, "ms": round(e2q_ms, 3), "pairs_per_s": round(P / (e2q_ms * 1e-3), 1), "batches": 8,
+            "statistic": "mean over a stream of 8 batches",
+            "note": "two AlignBatch objects in flight: batch i+1's pyramids build and its features go up (copy stream) "
+                    "while batch i aligns; then batch i's results come back and batch i+1 is queued"},
         "latency": lat,
         "batch_scaling": scaling_lines,
     }
