@@ -43,3 +43,22 @@ def test_bench_gpus2_spawns_two_ranks():
 def test_bench_rejects_world_size_mismatch():
     r = _run(["--gpus", "2"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in (r.stderr + r.stdout)
+
+
+def test_bench_chain_count_follows_the_library():
+    """bench.py's n_chains (the `roofline.kernel` text and the batch-scaling lines) restates run_batch's split rule;
+    the constants it restates are read from csrc/capi.hip so the two cannot drift apart."""
+    import re
+    sys.path.insert(0, ROOT)
+    import bench
+    import svo_amd
+    src = open(os.path.join(ROOT, "semi-direct-visual-odometry_amd", "csrc", "capi.hip")).read()
+    const = {k: int(re.search(rf"constexpr int(?:32_t)? {k} = (\d+);", src).group(1))
+             for k in ("kSplitMin", "kSplits", "kSplitsRefv", "kSplitsRefvMin")}
+    ref, exact = svo_amd.MEDIAN_REFERENCE, svo_amd.MEDIAN_EXACT
+    bench.svo_amd = svo_amd
+    assert bench.n_chains(const["kSplitMin"] - 1, ref) == 1
+    assert bench.n_chains(const["kSplitMin"], ref) == const["kSplits"]
+    assert bench.n_chains(const["kSplitsRefvMin"] - 1, ref) == const["kSplits"]
+    assert bench.n_chains(const["kSplitsRefvMin"], ref) == const["kSplitsRefv"]
+    assert bench.n_chains(const["kSplitsRefvMin"], exact) == const["kSplits"]
