@@ -1,6 +1,7 @@
 // align_refv.hip — K2V: the reference's robust scale bit for bit with the residual vector resident in one CU's
-// registers (median_mode SVO_MEDIAN_REFERENCE; three register layouts: LayA, vectors of <= 50 176 slots (the
-// config-2 shape), LayB, <= 60 416 slots, LayC, <= 65 024; K2R in align_ref.hip takes larger ones).
+// registers (median_mode SVO_MEDIAN_REFERENCE; two register layouts: LayA, vectors of <= 50 176 slots (the
+// config-2 shape), LayB, <= 60 416 slots; K2R in align_ref.hip takes larger ones: a third layout of 65 536 slots, whose
+// LDS rows left a mailbox small enough to chunk every large round, measured slower than K2R).
 //
 // What it reproduces: Optimizer::tukeyWeighting (src/optimizer.cpp:485-514) takes sigma = 1.4826 * MAD with
 // algorithm::computeMedian (src/algorithm.cpp:834-853) on the FULL residual vector (n_features * patch^2
@@ -73,9 +74,6 @@ struct Lay {
 };
 using LayA = Lay<RowsA, 98, 12288, true>;   // 50 176 slots: 88 register rows (v80..v255) + 10 LDS rows
 using LayB = Lay<RowsB, 118, 4352, false>;  // 60 416 slots: 92 register rows (v72..v255) + 26 LDS rows
-// 65 024 slots (2600 features at patch 5): 96 register rows (v64..v255) + 31 LDS rows; the LDS rows leave a 1856-swap
-// mailbox, so the large rounds exchange in chunks (LayB's kernel keeps its compiler code below v64)
-using LayC = Lay<RowsC, 127, 1856, false>;
 
 template <class L>
 struct VShared {
@@ -1258,7 +1256,6 @@ __global__ void __launch_bounds__(kVT, 1) align_scale_refv_kernel(AlignArgs a, i
 }
 template __global__ void align_scale_refv_kernel<LayA>(AlignArgs, int);
 template __global__ void align_scale_refv_kernel<LayB>(AlignArgs, int);
-template __global__ void align_scale_refv_kernel<LayC>(AlignArgs, int);
 
 // svo_debug_robust_scale: the same selection on an arbitrary vector (one workgroup); out[0..1] med / mad,
 // out[2..] diagnostics (rounds, chunked rounds, heap selects, cycles per pass)
@@ -1294,24 +1291,20 @@ __global__ void __launch_bounds__(kVT, 1) debug_robust_scale_v_kernel(const doub
     }
 }
 
-int64_t refv_max_slots() { return LayC::kCap; }
+int64_t refv_max_slots() { return LayB::kCap; }
 // the smaller layout (more mailbox, the MAD rows preloaded) whenever every pair of the launch fits it
 void launch_scale_refv(const AlignArgs& a, int level, hipStream_t s) {
     if ((uint32_t)a.max_slots <= LayA::kCap)
         hipLaunchKernelGGL(align_scale_refv_kernel<LayA>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
-    else if ((uint32_t)a.max_slots <= LayB::kCap)
-        hipLaunchKernelGGL(align_scale_refv_kernel<LayB>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
     else
-        hipLaunchKernelGGL(align_scale_refv_kernel<LayC>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
+        hipLaunchKernelGGL(align_scale_refv_kernel<LayB>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
 }
 void launch_debug_robust_scale_v(const double* v, uint32_t M, uint32_t n, double* gseg, double* out, double* trace,
                                  uint32_t trcap, hipStream_t s) {
     if (M <= LayA::kCap)
         hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayA>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
-    else if (M <= LayB::kCap)
-        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayB>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
     else
-        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayC>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
+        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayB>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
 }
 
 }  // namespace svo

@@ -1,7 +1,7 @@
 """Reference-mode batch time against the vector size (diagnostic): 256 pairs of nf features (patch 5, 5 levels,
 8 scenes), median of 5 runs after a warm-up (run + results, host clock).  The robust-scale kernel comes from
 SVO_SCALE_IMPL (unset: K2V where the vector fits its registers; 1: K2R), so run it once per setting:
-    python3 tools/k2v_large.py 2000 2400 2600"""
+    python3 tools/k2v_large.py 2000 2400 2600        (SVO_LIB_DIR=<a variant build>: another K2V library)"""
 import os
 import sys
 import time
