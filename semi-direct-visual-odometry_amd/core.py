@@ -1050,7 +1050,7 @@ def robust_scale_capacity(impl):
     v = ctypes.c_int64()
     check(lib().svo_robust_scale_capacity(int(impl), ctypes.byref(v)))
     return int(v.value)
-SCALE_K2V_MAX_SLOTS = 118 * 512             # K2V holds the vector in registers (align_refv.hip LayB)
+SCALE_K2V_MAX_SLOTS = 128 * 512             # K2V holds the vector in registers (align_refv.hip LayC)
 SCALE_K2V_LAYB_SLOTS = 118 * 512            # (LayB)
 SCALE_K2V_LAYA_SLOTS = 98 * 512             # (LayA: the faster layout, the config-2 shape)
 

@@ -1,7 +1,6 @@
 // align_refv.hip — K2V: the reference's robust scale bit for bit with the residual vector resident in one CU's
-// registers (median_mode SVO_MEDIAN_REFERENCE; two register layouts: LayA, vectors of <= 50 176 slots (the
-// config-2 shape), LayB, <= 60 416 slots; K2R in align_ref.hip takes larger ones: a third layout of 65 536 slots, whose
-// LDS rows left a mailbox small enough to chunk every large round, measured slower than K2R).
+// registers (median_mode SVO_MEDIAN_REFERENCE; three register layouts: LayA, vectors of <= 50 176 slots (the
+// config-2 shape), LayB, <= 60 416 slots, LayC, <= 65 536; K2R in align_ref.hip takes larger ones).
 //
 // What it reproduces: Optimizer::tukeyWeighting (src/optimizer.cpp:485-514) takes sigma = 1.4826 * MAD with
 // algorithm::computeMedian (src/algorithm.cpp:834-853) on the FULL residual vector (n_features * patch^2
@@ -74,6 +73,10 @@ struct Lay {
 };
 using LayA = Lay<RowsA, 98, 12288, true>;   // 50 176 slots: 88 register rows (v80..v255) + 10 LDS rows
 using LayB = Lay<RowsB, 118, 4352, false>;  // 60 416 slots: 92 register rows (v72..v255) + 26 LDS rows
+// 65 536 slots (2621 features at patch 5): 96 register rows (v64..v255) + 32 LDS rows; the LDS rows leave a 1344-swap
+// mailbox (163 032 of the CU's 163 840 LDS bytes in all), so the large rounds exchange in chunks, each walking only its
+// own steps (LayC's kernels keep their compiler code below v64)
+using LayC = Lay<RowsC, 128, 1344, false>;
 
 template <class L>
 struct VShared {
@@ -90,6 +93,7 @@ struct VShared {
     double lrow[L::kRows - L::kRegRows][kVT];  // the LDS rows of the vector (the rest is in registers)
     uint32_t tmp[2 * kVW];            // per-wave counts of the prologue
 };
+static_assert(sizeof(VShared<LayC>) <= 163840, "LayC's shared state fits the CU's LDS");
 
 struct VDiag {  // svo_debug_robust_scale diagnostics
     uint32_t nblock[2], nwave[2], heap[2], nchunk[2];
@@ -185,6 +189,9 @@ struct VSel {
 #define SVO_FEWROWS 8
 #endif
     static constexpr int kFewRows = SVO_FEWROWS;
+    // chunked rounds walk each chunk's own steps (LayB / LayC, whose 4352- / 1344-swap mailboxes chunk the large
+    // rounds; LayA's 12 288 swaps chunk none of the config-2 shape's, and the extra searches push its code past v80)
+    static constexpr bool kChunkSteps = kMbCap < 12288;
 #ifndef SVO_QG
 #define SVO_QG 4
 #endif
@@ -525,6 +532,21 @@ struct VSel {
         const uint32_t s = find_step(C, kind, rank, pre);
         return s * 64u + wave_select_bit(rec_mask(s, kind), rank - kval(pre, kind) - 1u);
     }
+    // locate() reading the row's per-step counts back from LDS instead of the Ctl registers (the chunked exchange's
+    // searches: the sixteen count registers would otherwise stay live through the chunk loop and push the code past
+    // the VGPR fence)
+    __device__ __forceinline__ uint32_t locate_lds(const Ctl& C, int kind, uint32_t rank) const {
+        const uint32_t n = popc(__ballot(kval(C.rp[0], kind) < rank)) + popc(__ballot(kval(C.rp[1], kind) < rank));
+        const uint32_t jr = n - 1u, g = jr >> 6, ln = jr & 63u;
+        uint32_t pk = uni(lane_read(g ? C.rp[1] : C.rp[0], (int)ln)), st = 0, p0 = pk;
+#pragma unroll
+        for (int u = 0; u < kVW; ++u) {
+            if (kval(pk, kind) < rank) { st = (uint32_t)u; p0 = pk; }
+            pk += uni(sh.cnt[u][jr]);
+        }
+        const uint32_t s = jr * kVW + st;
+        return s * 64u + wave_select_bit(rec_mask(s, kind), rank - kval(p0, kind) - 1u);
+    }
     // the j-th (0-based) set bit of a uniform mask: the lane holding it has j set bits below it
     __device__ __forceinline__ uint32_t wave_select_bit(uint64_t m, uint32_t j) const {
         const uint64_t hit = __ballot(((m >> lane) & 1ull) && lanes_below(m) == j);
@@ -846,11 +868,31 @@ struct VSel {
         const uint32_t nch = ks == 0 ? 1u : (ks + kMbCap - 1u) / kMbCap;
         uint32_t ck[4] = {0, 0, 0, 0};  // the candidates' target ranks (0: not a target)
         VSTAMP(3);
+        // a chunk's steps on one side: the positions of its ranks (k0, k1] (side 0: GE ranked from the left, L_k;
+        // side 1: LE ranked from the right, R_k) are contiguous, so a chunk walks only the steps from its first to its
+        // last rank's instead of the side's whole range (a chunked round then visits each row about once, not nch times)
+        auto chunk_steps = [&](int side, uint32_t k0, uint32_t k1, uint32_t& s0, uint32_t& s1) __attribute__((always_inline)) {
+            if (side == 0) {
+                s0 = uni(locate_lds(C, 0, k0 + 1u)) >> 6;
+                s1 = uni(locate_lds(C, 0, k1)) >> 6;
+            } else {
+                s0 = uni(locate_lds(C, 1, C.totL - k1 + 1u)) >> 6;
+                s1 = uni(locate_lds(C, 1, C.totL - k0)) >> 6;
+            }
+        };
         for (uint32_t it = 0; it < nch; ++it) {
             const uint32_t k0 = it * kMbCap, k1 = ks < k0 + kMbCap ? ks : k0 + kMbCap;
             if (ks) {
-                if (src_side == 0) exchange<true>(C, 0, s0L, s1L, s1L, p, k0, k1, nch > 1);
-                else exchange<true>(C, 1, s0R, s1R, s0R, p, k0, k1, nch > 1);
+                if (kChunkSteps && nch > 1) {
+                    uint32_t c0, c1;
+                    chunk_steps(src_side, k0, k1, c0, c1);
+                    if (src_side == 0) exchange<true>(C, 0, c0, c1, c1, p, k0, k1, true);
+                    else exchange<true>(C, 1, c0, c1, c0, p, k0, k1, true);
+                } else if (src_side == 0) {
+                    exchange<true>(C, 0, s0L, s1L, s1L, p, k0, k1, nch > 1);
+                } else {
+                    exchange<true>(C, 1, s0R, s1R, s0R, p, k0, k1, nch > 1);
+                }
             }
             VSTAMP(4);
             __syncthreads();
@@ -866,8 +908,16 @@ struct VSel {
                 }
             }
             if (ks) {
-                if (tgt_side == 0) exchange<false>(C, 0, s0L, s1L, s1L, p, k0, k1, nch > 1);
-                else exchange<false>(C, 1, s0R, s1R, s0R, p, k0, k1, nch > 1);
+                if (kChunkSteps && nch > 1) {
+                    uint32_t c0, c1;
+                    chunk_steps(tgt_side, k0, k1, c0, c1);
+                    if (tgt_side == 0) exchange<false>(C, 0, c0, c1, c1, p, k0, k1, true);
+                    else exchange<false>(C, 1, c0, c1, c0, p, k0, k1, true);
+                } else if (tgt_side == 0) {
+                    exchange<false>(C, 0, s0L, s1L, s1L, p, k0, k1, nch > 1);
+                } else {
+                    exchange<false>(C, 1, s0R, s1R, s0R, p, k0, k1, nch > 1);
+                }
                 if (need) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
@@ -1256,6 +1306,7 @@ __global__ void __launch_bounds__(kVT, 1) align_scale_refv_kernel(AlignArgs a, i
 }
 template __global__ void align_scale_refv_kernel<LayA>(AlignArgs, int);
 template __global__ void align_scale_refv_kernel<LayB>(AlignArgs, int);
+template __global__ void align_scale_refv_kernel<LayC>(AlignArgs, int);
 
 // svo_debug_robust_scale: the same selection on an arbitrary vector (one workgroup); out[0..1] med / mad,
 // out[2..] diagnostics (rounds, chunked rounds, heap selects, cycles per pass)
@@ -1291,20 +1342,24 @@ __global__ void __launch_bounds__(kVT, 1) debug_robust_scale_v_kernel(const doub
     }
 }
 
-int64_t refv_max_slots() { return LayB::kCap; }
+int64_t refv_max_slots() { return LayC::kCap; }
 // the smaller layout (more mailbox, the MAD rows preloaded) whenever every pair of the launch fits it
 void launch_scale_refv(const AlignArgs& a, int level, hipStream_t s) {
     if ((uint32_t)a.max_slots <= LayA::kCap)
         hipLaunchKernelGGL(align_scale_refv_kernel<LayA>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
-    else
+    else if ((uint32_t)a.max_slots <= LayB::kCap)
         hipLaunchKernelGGL(align_scale_refv_kernel<LayB>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
+    else
+        hipLaunchKernelGGL(align_scale_refv_kernel<LayC>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
 }
 void launch_debug_robust_scale_v(const double* v, uint32_t M, uint32_t n, double* gseg, double* out, double* trace,
                                  uint32_t trcap, hipStream_t s) {
     if (M <= LayA::kCap)
         hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayA>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
-    else
+    else if (M <= LayB::kCap)
         hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayB>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
+    else
+        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayC>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
 }
 
 }  // namespace svo

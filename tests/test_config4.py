@@ -159,8 +159,7 @@ def test_gpu_scale_kernel_follows_the_frame():
     ia = svo_amd.ImageAlignment(PATCH, 0, L - 1, ctx=ctx)
     scenes = {nf: synth.make_pair(seed=synth.SEED_BASE + 900 + nf, n_features=nf, patch_size=PATCH)
               for nf in (2000, 2400, 2600, 2621)}
-    # 2000 -> LayA, 2400 -> LayB (K2V at every level), 2600 (65 000 slots) and 2621 (65 525) -> K2R at every level: a
-    # 65 536-slot K2V layout measured slower than K2R there
+    # 2000 -> LayA, 2400 -> LayB, 2600 (65 000 slots) and 2621 (65 525) -> LayC: K2V at every level
     for nf in (2000, 2400, 2600, 2621, 2000):
         s = scenes[nf]
         ref, cur = _class_frames(s, ctx)

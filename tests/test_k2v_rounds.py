@@ -30,7 +30,7 @@ def residual_like(ns, seed, vis=0.8, ints=False):
     return v, int((v < DBL_MAX).sum())
 
 
-FAMILIES = [("normal", 50000, 1, 0.8, False), ("normal", 60000, 1, 0.8, False), ("normal", 50176, 3, 1.0, False),
+FAMILIES = [("normal", 50000, 1, 0.8, False), ("normal", 60000, 1, 0.8, False), ("normal", 65000, 8, 0.8, False), ("normal", 65536, 9, 0.9, False), ("normal", 50176, 3, 1.0, False),
             ("integers", 50000, 4, 0.9, True), ("normal", 12000, 5, 0.7, False), ("integers", 3000, 6, 1.0, True),
             ("normal", 700, 7, 0.8, False)]
 

@@ -1,7 +1,7 @@
 """Build-time check of K2V's register fences (semi-direct-visual-odometry_amd/csrc/align_refv.hip).
 
 K2V keeps the register rows of each pair's residual vector in the VGPRs above its layout's fence (v80..v255 for
-LayA, v72..v255 for LayB), written and read only by its inline-asm blocks.  The compiler is not told about them
+LayA, v72..v255 for LayB, v64..v255 for LayC), written and read only by its inline-asm blocks.  The compiler is not told about them
 outside those blocks, so this check reads the generated assembly of every K2V kernel instantiation, from its
 entry label to its .Lfunc_end label, takes the fence from the kernel's `;@vfence B` marker, and fails when
 

@@ -2,10 +2,11 @@
 
 K2V (csrc/align_refv.hip) keeps the residual vector of one pair in the VGPRs of one CU: row r < kRegRows of
 every lane in the pair v[B + 2r : B + 2r + 1] above a register fence B (the compiler's own values stay below
-it), the remaining rows in LDS.  Two layouts, one struct each:
+it), the remaining rows in LDS.  Three layouts, one struct each:
 
   RowsA  B = 80, 88 register rows   (K2V's 98-row layout: vectors of <= 50 176 slots, the config-2 shape)
   RowsB  B = 72, 92 register rows   (the 118-row layout: <= 60 416 slots, frames of up to 2416 features at patch 5)
+  RowsC  B = 64, 96 register rows   (the 128-row layout: <= 65 536 slots, frames of up to 2621 features at patch 5)
 
 Every struct holds
   load(src, bytes, tid) / mad(med) / unstage(a)   the rows' buffer loads, the MAD pass's |x - med| in place, and
@@ -44,7 +45,7 @@ usage: python3 tools/gen_refv_rows.py [out]  (writes the header; the output is c
 """
 import os
 
-LAYOUTS = (("RowsA", 80), ("RowsB", 72))
+LAYOUTS = (("RowsA", 80), ("RowsB", 72), ("RowsC", 64))
 # the quads' instruction-level parallelism form (cls4_ilp / exch_ilp): compares first, then independent per-row chains
 ILP = os.environ.get("SVO_GEN_ILP", "1") == "1"
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "semi-direct-visual-odometry_amd",
