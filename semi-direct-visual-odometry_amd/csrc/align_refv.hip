@@ -210,6 +210,7 @@ struct VSel {
     int tid, lane, wave;
     // block-uniform selection state
     uint32_t f, l;
+    uint32_t xk0 = 0, xk1 = 0;  // the exchange's current rank window (k0, k1] (a chunk's, or (0, Ks])
     int depth;
     bool rec;
     double lo_val;
@@ -621,7 +622,8 @@ struct VSel {
             else if ((okm >> lane) & 1ull) sh.lrow[r - kVRegRows][tid] = t;
         }
     }
-    // (one chunk: k0 = 0) rows ra..rb of this wave; pb[g]: lane j the mailbox byte address of row 64 g + j's slot 0
+    // rows ra..rb of this wave; pb[g]: lane j the mailbox byte address of row 64 g + j's slot 0 (of the chunk's ranks
+    // (xk0, xk1], which the LDS rows' generic path tests)
     template <int Q, bool kWrite, int S>
     __device__ __forceinline__ void ex_quad(const Ctl& C, double p, int ra, int rb, const uint32_t (&pb)[2]) {
         opaque(ra, rb);
@@ -639,7 +641,7 @@ struct VSel {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = 4 * Q + i;
-                if (r < R && r >= ra && r <= rb) generic_row<kWrite>(C, S, r, ~0ull, p, 0u, kMbCap, false);
+                if (r < R && r >= ra && r <= rb) generic_row<kWrite>(C, S, r, ~0ull, p, xk0, xk1, false);
             }
         }
     }
@@ -654,13 +656,13 @@ struct VSel {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int r = 4 * Q + i;
-                if (r < R) generic_row<kWrite>(C, S, r, ~0ull, p, 0u, kMbCap, false);
+                if (r < R) generic_row<kWrite>(C, S, r, ~0ull, p, xk0, xk1, false);
             }
         }
     }
     template <bool kWrite, int S>
-    __device__ __forceinline__ void ex_quads(const Ctl& C, double p, int ra, int rb) {
-        const uint32_t mb = (uint32_t)(uintptr_t)sh.mbx;
+    __device__ __forceinline__ void ex_quads(const Ctl& C, double p, int ra, int rb, uint32_t k0) {
+        const uint32_t mb = (uint32_t)(uintptr_t)sh.mbx - 8u * k0;  // (a chunk's ranks (k0, k1] in slots 0 ..)
         uint32_t pb[2];
 #pragma unroll
         for (int g = 0; g < 2; ++g)
@@ -698,24 +700,28 @@ struct VSel {
         const WaveRows w = wave_segment(s0, s1);
         if (w.rlo > w.rhi) return;
         const uint64_t gfirst = side == 0 ? w.ge_first : w.le_first;
-        if (chunked) {  // (rare: more than kMbCap swaps) every row the generic way, masks from the records
+        if (chunked && !kChunkSteps) {  // (LayA: never for the config-2 shape) every row generic, masks from the records
             for (int r = w.rlo; r <= w.rhi; ++r)
                 generic_row<kWrite>(C, side, r, r == w.rlo ? gfirst : (r == w.rhi ? w.last : ~0ull), p, k0, k1, true);
             return;
         }
-        generic_row<kWrite>(C, side, w.rlo, w.rlo == w.rhi ? gfirst & w.last : gfirst, p, k0, k1, false);
-        if (w.rhi > w.rlo) generic_row<kWrite>(C, side, w.rhi, w.last, p, k0, k1, false);
-        // (the rank boundary L_Ks / R_Ks lies in the first step of side 1's range or the last of side 0's, so its row
-        // is always an end row of the wave that owns the step: the interior rows need no rank test)
+        // (a chunk's end rows take their masks from the records: an earlier chunk's targets may sit in its first or
+        // last step; every step between holds only this chunk's ranks and rows no earlier chunk touched)
+        generic_row<kWrite>(C, side, w.rlo, w.rlo == w.rhi ? gfirst & w.last : gfirst, p, k0, k1, chunked);
+        if (w.rhi > w.rlo) generic_row<kWrite>(C, side, w.rhi, w.last, p, k0, k1, chunked);
+        // (the rank boundaries (L_Ks / R_Ks, or a chunk's first and last ranks) lie in the first / last step of the
+        // range, so their rows are end rows of the waves that own those steps: the interior rows need no rank test)
         (void)bstep;
         const int ra = w.rlo + 1, rb = w.rhi - 1;
         if (ra > rb) return;
         if (rb - ra < kFewRows) {  // a few rows: the generic way, no pass over every quad's range test
-            for (int r = ra; r <= rb; ++r) generic_row<kWrite>(C, side, r, ~0ull, p, 0u, kMbCap, false);
+            for (int r = ra; r <= rb; ++r) generic_row<kWrite>(C, side, r, ~0ull, p, k0, k1, false);
             return;
         }
-        if (side == 0) ex_quads<kWrite, 0>(C, p, ra, rb);
-        else ex_quads<kWrite, 1>(C, p, ra, rb);
+        xk0 = k0;
+        xk1 = k1;
+        if (side == 0) ex_quads<kWrite, 0>(C, p, ra, rb, k0);
+        else ex_quads<kWrite, 1>(C, p, ra, rb, k0);
     }
 
     // ------------------------------------------------------------------ one block round
