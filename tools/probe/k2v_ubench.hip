@@ -116,6 +116,25 @@ __global__ void __launch_bounds__(1024) ubench(double* io, uint64_t* cyc, uint32
 #pragma unroll
             for (int i = 0; i < 4; ++i) s = (uint32_t)__builtin_amdgcn_readlane((int)(a0 + s), (int)(s & 63)) + 1u;
             acc = s;
+        } else if constexpr (V == 7) {  // four indexed-register reads (s_set_gpr_idx_on SRC0 / v_mov / off), K2V's vget
+            uint32_t lo0, lo1, lo2, lo3;
+            const uint32_t i0 = (acc & 3u) * 2u, i1 = ((acc + 1u) & 3u) * 2u, i2 = ((acc + 2u) & 3u) * 2u, i3 = ((acc + 3u) & 3u) * 2u;
+            asm volatile("s_set_gpr_idx_on %4, gpr_idx(SRC0)\n\tv_mov_b32 %0, %8\n\ts_set_gpr_idx_off\n\t"
+                         "s_set_gpr_idx_on %5, gpr_idx(SRC0)\n\tv_mov_b32 %1, %8\n\ts_set_gpr_idx_off\n\t"
+                         "s_set_gpr_idx_on %6, gpr_idx(SRC0)\n\tv_mov_b32 %2, %8\n\ts_set_gpr_idx_off\n\t"
+                         "s_set_gpr_idx_on %7, gpr_idx(SRC0)\n\tv_mov_b32 %3, %8\n\ts_set_gpr_idx_off"
+                         : "=&v"(lo0), "=&v"(lo1), "=&v"(lo2), "=&v"(lo3)
+                         : "s"(__builtin_amdgcn_readfirstlane(i0)), "s"(__builtin_amdgcn_readfirstlane(i1)),
+                           "s"(__builtin_amdgcn_readfirstlane(i2)), "s"(__builtin_amdgcn_readfirstlane(i3)),
+                           "v"((uint32_t)__builtin_bit_cast(uint64_t, x0)));
+            acc += lo0 ^ lo1 ^ lo2 ^ lo3;
+        } else if constexpr (V == 8) {  // the same four reads on fixed registers (plain v_mov)
+            uint32_t lo0, lo1, lo2, lo3;
+            asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"
+                         : "=&v"(lo0), "=&v"(lo1), "=&v"(lo2), "=&v"(lo3)
+                         : "v"((uint32_t)__builtin_bit_cast(uint64_t, x0)), "v"((uint32_t)__builtin_bit_cast(uint64_t, x1)),
+                           "v"((uint32_t)__builtin_bit_cast(uint64_t, x2)), "v"((uint32_t)__builtin_bit_cast(uint64_t, x3)));
+            acc += lo0 ^ lo1 ^ lo2 ^ lo3;
         } else if constexpr (V == 6) {  // LDS write -> read round trip (uniform address)
             mb[(acc & 1023u) + 64u * wave] = x0;
             asm volatile("" ::: "memory");
@@ -142,10 +161,10 @@ int main() {
     (void)hipMemcpy(io, h, sizeof(h), hipMemcpyHostToDevice);
     const char* names[] = {"cls quad, round-4 serial (VCC)", "cls quad, compares first + writelanes",
                            "8 compares only", "src quad, round-4 serial", "src quad, independent chains",
-                           "readlane->SALU->readlane", "LDS write->read"};
+                           "readlane->SALU->readlane", "LDS write->read", "4 indexed reads (gpr_idx)", "4 fixed v_mov"};
     void (*ks[])(double*, uint64_t*, uint32_t*) = {ubench<0>, ubench<1>, ubench<2>, ubench<3>, ubench<4>, ubench<5>,
-                                                   ubench<6>};
-    for (int v = 0; v < 7; ++v) {
+                                                   ubench<6>, ubench<7>, ubench<8>};
+    for (int v = 0; v < 9; ++v) {
         for (int nw : {1, 4, 8, 16}) {
             hipLaunchKernelGGL(ks[v], dim3(1), dim3(64 * nw), 0, 0, io, cyc, sink);  // warm
             hipLaunchKernelGGL(ks[v], dim3(1), dim3(64 * nw), 0, 0, io, cyc, sink);
