@@ -28,8 +28,8 @@
 //      vec[nth - 1] need; the sources write the mailbox (LDS, slot k - 1), EXEC set to the row's side mask;  barrier
 //   3. the kept side's targets take the mailbox values (EXEC-masked moves into the rows); all read the next
 //      pivot's candidates.
-// A mailbox larger than the layout's kMbCap swaps runs in chunks.  Segments of <= 512 continue on wave 0 in its
-// rows 0..7 without barriers; the depth limit falls back to the restated heap select (adversarial inputs only).
+// A mailbox larger than the layout's kMbCap swaps runs in chunks.  Segments of <= 1024 (LayC: 512) continue on wave 0 in
+// its rows 0..15 (0..7) without barriers; the depth limit falls back to the restated heap select (adversarial inputs only).
 // No global traffic but the two reads of K1's residuals per pair and level (one per pass).
 #include "svo_internal.h"
 #include "svo_math.h"
@@ -46,10 +46,12 @@ using namespace refsel;
 
 constexpr int kVT = 512;              // threads per pair
 constexpr int kVW = kVT / 64;         // waves
-constexpr uint32_t kOneWave = 512;    // segments of <= kOneWave positions continue on wave 0 (its rows 0..7)
-// wave 0's register rows for the MAD pass, staged by the other waves during its one-wave rounds, past the one-wave
-// segment and its mailbox
-constexpr uint32_t kStage = 2 * kOneWave;
+// segments of <= OW positions (a layout's one-wave size, a multiple of 256: 1024 for LayA / LayB, 512 for LayC, whose
+// mailbox holds no more) continue on wave 0 (its rows 0 .. OW / 64 - 1); wave 0's register rows for the MAD pass are staged by the other waves during its one-wave rounds
+// past the one-wave segment and its mailbox (mbx[2 OW, ...))
+#ifndef SVO_ONEWAVE
+#define SVO_ONEWAVE 1024
+#endif
 constexpr int kRowPad = 128;          // record planes: rows padded to two groups of 64 lanes
 
 #include "refv_rows.h"
@@ -57,7 +59,7 @@ constexpr int kRowPad = 128;          // record planes: rows padded to two group
 // A register layout: G the data registers (refv_rows.h: rows 0 .. G::kRegRows - 1 above G::kBase), R rows in all
 // (the rest in LDS), a mailbox of MB doubles (Ks beyond it exchanges in chunks), PRE: the MAD pass's rows load
 // during the median pass's one-wave rounds (staged in the mailbox).
-template <class G, int R, uint32_t MB, bool PRE>
+template <class G, int R, uint32_t MB, bool PRE, uint32_t OW>
 struct Lay {
     using Rows = G;
     static constexpr int kRows = R;
@@ -65,22 +67,25 @@ struct Lay {
     static constexpr uint32_t kMbCap = MB;
     static constexpr bool kPreload = PRE;
     static constexpr uint32_t kCap = (uint32_t)R * kVT;
+    static constexpr uint32_t kOneWave = OW;
+    static constexpr uint32_t kStage = 2 * OW;
+    static_assert(OW % 256 == 0 && OW / 64 <= G::kRegRows && OW <= 4096, "one-wave rows: register quads of wave 0");
     static_assert(R > G::kRegRows && R <= kRowPad, "rows");
-    static_assert(2 * kOneWave <= MB && MB % 64 == 0, "one-wave segment and its mailbox");
+    static_assert(2 * OW <= MB && MB % 64 == 0, "one-wave segment and its mailbox");
     static_assert(!PRE || kStage + 64 * G::kRegRows <= MB, "staging of wave 0's rows inside the mailbox");
     // stage_wave0: waves 1..7 take rows wave - 1 + 7 i, i < R / 7, which reaches every row only for R a multiple of 7
     static_assert(!PRE || R % (kVW - 1) == 0, "stage_wave0 covers every row");
 };
-using LayA = Lay<RowsA, 98, 12288, true>;   // 50 176 slots: 88 register rows (v80..v255) + 10 LDS rows
-using LayB = Lay<RowsB, 118, 4352, false>;  // 60 416 slots: 92 register rows (v72..v255) + 26 LDS rows
+using LayA = Lay<RowsA, 98, 12288, true, SVO_ONEWAVE>;   // 50 176 slots: 88 register rows (v80..v255) + 10 LDS rows
+using LayB = Lay<RowsB, 118, 4352, false, SVO_ONEWAVE>;  // 60 416 slots: 92 register rows (v72..v255) + 26 LDS rows
 // 65 536 slots (2621 features at patch 5): 96 register rows (v64..v255) + 32 LDS rows; the LDS rows leave a 1344-swap
 // mailbox (163 032 of the CU's 163 840 LDS bytes in all), so the large rounds exchange in chunks, each walking only its
 // own steps (LayC's kernels keep their compiler code below v64)
-using LayC = Lay<RowsC, 128, 1344, false>;
+using LayC = Lay<RowsC, 128, 1344, false, 512>;
 
 template <class L>
 struct VShared {
-    // mailbox (mbx[0, kMbCap); the one-wave segment in [0, 512) and its mailbox in [512, 1024)), then the
+    // mailbox (mbx[0, kMbCap); the one-wave segment in [0, OW) and its mailbox in [OW, 2 OW)), then the
     // per-lane dummy slots of the generic exchange rows (mbx[kMbCap + lane]): one array, so a lane's slot is
     // one selected index
     double mbx[L::kMbCap + 64];
@@ -112,7 +117,7 @@ struct VDiag {  // svo_debug_robust_scale diagnostics
 #endif
     // round trace (svo_debug_robust_scale with out_len > 206; development): after every round a record of
     // kTrHead doubles (pass + 10 kind (0 block, 1 one-wave), f, l before the round, pivot, Ks, #GE, #LE, cut)
-    // and the vector's M slots (a one-wave round: only its 512 segment slots)
+    // and the vector's M slots (a one-wave round: only its segment slots)
     double* tr;
     uint32_t trcap, ntr;
 };
@@ -183,6 +188,8 @@ struct VSel {
     static constexpr int kVRegRows = L::kRegRows;
     static constexpr int kGenQuads = G::kGenQuads;
     static constexpr uint32_t kMbCap = L::kMbCap;
+    static constexpr uint32_t kOneWave = L::kOneWave;
+    static constexpr uint32_t kStage = L::kStage;
     static constexpr int kQuads = (R + 3) / 4;  // quads of rows the block rounds walk (kGenQuads of them in registers)
     // below this many rows a wave classifies and exchanges row by row (indexed registers) instead of walking the quads
 #ifndef SVO_FEWROWS
@@ -748,10 +755,12 @@ struct VSel {
         const uint32_t i = dg->ntr;
         if ((uint64_t)(i + 1u) * (kTrHead + M) > dg->trcap) return nullptr;
         double* const b = dg->tr + (uint64_t)i * (kTrHead + M);
-        if (tid == 0) {
-            const double h[kTrHead] = {(double)(P + 10 * (int)kind), (double)f0, (double)l0, p, (double)ks, (double)tg,
-                                       (double)tl, (double)cut};
-            for (uint32_t j = 0; j < kTrHead; ++j) b[j] = h[j];
+        // one header field per lane of threads 0..7 (wave 0): a register pair, not the whole header, stays live
+        if (tid < (int)kTrHead) {
+            const uint32_t j = (uint32_t)tid;
+            const uint32_t u = j == 0 ? (uint32_t)(P + 10 * (int)kind) : j == 1 ? f0 : j == 2 ? l0 : j == 4 ? ks
+                             : j == 5 ? tg : j == 6 ? tl : cut;
+            b[j] = j == 3 ? p : (double)u;
         }
         return b + kTrHead;
     }
@@ -953,7 +962,7 @@ struct VSel {
     }
 
     // ------------------------------------------------------------------ rounds of <= 512 positions (wave 0)
-    // No barriers: wave 0 takes the segment (seg[i] = position f0 + i, from the dump) into its data rows 0..7
+    // No barriers: wave 0 takes the segment (seg[i] = position f0 + i, from the dump) into its data rows 0 .. OW / 64 - 1
     // (position f0 + 64 j + L in lane L of row j; the rows' own values are dead after the dump), so a round
     // reads no segment memory: the candidates are readlanes; the classification is cls4's compares with the masks
     // in lane j of four accumulators (row j = lane j), the packed counts and their prefixes one DPP scan, the
@@ -962,6 +971,25 @@ struct VSel {
     // then the rows go back to seg for the final sort or the heap select.
     __device__ __forceinline__ double cand_at(uint32_t q) const {
         return uni(lane_read(vget((int)(q >> 6)), (int)(q & 63u)));
+    }
+    // the one-wave round's quads of rows (Q = 0 .. kOneWave / 256 - 1) that meet rows [js, je]
+    template <int Q>
+    static __device__ __forceinline__ void w1_cls(double pe, uint32_t (&acc)[4], int js, int je) {
+        if constexpr (Q < (int)(kOneWave / 256)) {
+            if (js <= 4 * Q + 3 && je >= 4 * Q) G::template cls4<Q>(pe, acc);
+            w1_cls<Q + 1>(pe, acc, js, je);
+        }
+    }
+    template <int Q, int S, bool W>
+    static __device__ __forceinline__ void w1_ex(uint32_t ml, uint32_t mh, uint32_t pkv, uint32_t ks, uint32_t tl1,
+                                                 uint32_t mbb, int js, int je) {
+        if constexpr (Q < (int)(kOneWave / 256)) {
+            if (js <= 4 * Q + 3 && je >= 4 * Q) {
+                if constexpr (W) G::template w1src<Q, S>(ml, mh, pkv, ks, tl1, mbb);
+                else G::template w1tgt<Q, S>(ml, mh, pkv, ks, tl1, mbb);
+            }
+            w1_ex<Q + 1, S, W>(ml, mh, pkv, ks, tl1, mbb, js, je);
+        }
     }
     __device__ __forceinline__ void wave_rounds(double* seg, double* mb, uint32_t& nrounds) {
         const uint32_t f0 = f, me = (uint32_t)lane;
@@ -984,8 +1012,7 @@ struct VSel {
             int js = (int)(fr >> 6), je = (int)((lr - 1) >> 6);
             uint32_t acc[4] = {0, 0, 0, 0};  // lane j: row j's GE lo, GE hi, LE lo, LE hi
             opaque(js, je);
-            if (js <= 3) G::template cls4<0>(pe, acc);
-            if (je >= 4) G::template cls4<1>(pe, acc);
+            w1_cls<0>(pe, acc, js, je);
             // the rows' parts inside [fr, lr) (GE without the pivot at fr)
             const bool live = (int)me >= js && (int)me <= je;
             const uint32_t rb0 = 64u * me;
@@ -1038,15 +1065,11 @@ struct VSel {
             if (ks) {
                 const uint32_t tl1 = tL - 1u;
                 if (right) {
-                    if (js <= 3) G::template w1src<0, 0>(acc[0], acc[1], pkv, ks, tl1, mbb);
-                    if (je >= 4) G::template w1src<1, 0>(acc[0], acc[1], pkv, ks, tl1, mbb);
-                    if (js <= 3) G::template w1tgt<0, 1>(acc[2], acc[3], pkv, ks, tl1, mbb);
-                    if (je >= 4) G::template w1tgt<1, 1>(acc[2], acc[3], pkv, ks, tl1, mbb);
+                    w1_ex<0, 0, true>(acc[0], acc[1], pkv, ks, tl1, mbb, js, je);
+                    w1_ex<0, 1, false>(acc[2], acc[3], pkv, ks, tl1, mbb, js, je);
                 } else {
-                    if (js <= 3) G::template w1src<0, 1>(acc[2], acc[3], pkv, ks, tl1, mbb);
-                    if (je >= 4) G::template w1src<1, 1>(acc[2], acc[3], pkv, ks, tl1, mbb);
-                    if (js <= 3) G::template w1tgt<0, 0>(acc[0], acc[1], pkv, ks, tl1, mbb);
-                    if (je >= 4) G::template w1tgt<1, 0>(acc[0], acc[1], pkv, ks, tl1, mbb);
+                    w1_ex<0, 1, true>(acc[2], acc[3], pkv, ks, tl1, mbb, js, je);
+                    w1_ex<0, 0, false>(acc[0], acc[1], pkv, ks, tl1, mbb, js, je);
                 }
             }
             if (tracing()) {  // (wave 0 only: no barrier; the record counter is wave 0's)

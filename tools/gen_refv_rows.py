@@ -24,8 +24,8 @@ v_readfirstlane).
   src4<Q, S>(p, pb) / src4e<Q, S>(p, pb, ra, len)   the sources of an exchange write the mailbox   (side S)
   tgt4<Q, S>(p, pb) / tgt4e<Q, S>(p, pb, ra, len)   the targets take the mailbox values            (side S)
                                       (the e forms test each row against the row range [ra, ra + len])
-  w1src / w1tgt<Q, S>(ml, mh, pre, ks, tl1, mb)   rows 4Q..4Q+3 (< 8) of a one-wave round's exchange (wave 0,
-                                      the segment in its rows 0..7): sources / targets
+  w1src / w1tgt<Q, S>(ml, mh, pre, ks, tl1, mb)   rows 4Q..4Q+3 (< 32) of a one-wave round's exchange (wave 0,
+                                      the segment in its rows 0 .. OW / 64 - 1): sources / targets
   fence()                             the marker `;@vfence B` the build check reads in each kernel
 
 Every per-row decision of the quads happens inside the asm block, so the compiler has nothing to hoist across
@@ -46,6 +46,8 @@ usage: python3 tools/gen_refv_rows.py [out]  (writes the header; the output is c
 import os
 
 LAYOUTS = (("RowsA", 80), ("RowsB", 72), ("RowsC", 64))
+# the one-wave rounds' quads (rows 0 .. 4 W1QUADS - 1 of wave 0: one-wave segments of up to 256 W1QUADS positions)
+W1QUADS = 8
 # the quads' instruction-level parallelism form (cls4_ilp / exch_ilp): compares first, then independent per-row chains
 ILP = os.environ.get("SVO_GEN_ILP", "1") == "1"
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "semi-direct-visual-odometry_amd",
@@ -325,7 +327,7 @@ class Gen:
             for o in range(self.rows // 8):
                 for s in (0, 1):
                     out.append(self.exch(o, s, False, False, nr=8))
-        for q in range(2):
+        for q in range(W1QUADS):
             for s in (0, 1):
                 out.append(self.w1quad(q, s, True))
                 out.append(self.w1quad(q, s, False))
