@@ -283,8 +283,53 @@ class Gen:
                 f"    asm volatile(\"{asm(L)}\"\n                 : {', '.join(outs)}\n                 : {', '.join(ins)}\n"
                 f"                 : \"memory\", \"scc\");\n}}\n")
 
+    def w1quad_ilp(self, q, side):
+        # the four rows side by side: the masks and prefixes come from the compiler's readlanes (C++, before the block;
+        # the asm syntax cannot name one half of an SGPR pair), then the ranks (mbcnt over the mask halves, no EXEC
+        # change), the compares with Ks into their own SGPR pairs, the addresses, and only then the exec-masked LDS
+        # accesses (the reads all in flight together)
+        rows = list(range(4 * q, 4 * q + 4))
+        pro = []
+        for i, j in enumerate(rows):
+            pro += [f"    const uint64_t m{i} = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(mh, {j}) << 32) | "
+                    f"(uint32_t)__builtin_amdgcn_readlane(ml, {j});"]
+            pro += [f"    const uint32_t t{i} = __builtin_amdgcn_readlane(pre, {j}) & 0xFFFFu;" if side == 0 else
+                    f"    const uint32_t t{i} = tl1 - (__builtin_amdgcn_readlane(pre, {j}) >> 16);"]
+        L = [f"v_mbcnt_lo_u32_b32 %[k{i}], %[ml{i}], 0" for i in range(4)]
+        L += [f"v_mbcnt_hi_u32_b32 %[k{i}], %[mh{i}], %[k{i}]" for i in range(4)]
+        L += [(f"v_add_u32 %[k{i}], %[t{i}], %[k{i}]" if side == 0 else f"v_sub_u32 %[k{i}], %[t{i}], %[k{i}]")
+              for i in range(4)]
+        L += [f"v_cmp_gt_u32_e64 %[c{i}], %[ks], %[k{i}]" for i in range(4)]
+        L += [f"v_lshl_add_u32 %[k{i}], %[k{i}], 3, %[mb]" for i in range(4)]
+        L += [f"s_and_b64 %[c{i}], %[c{i}], %[m{i}]" for i in range(4)]
+        return pro, L
+
     def w1quad(self, q, side, write):
         rows = list(range(4 * q, 4 * q + 4))
+        if ILP:
+            pro, L = self.w1quad_ilp(q, side)
+            L.append("s_mov_b64 %[sv], exec")
+            for i, j in enumerate(rows):
+                L += [f"s_mov_b64 exec, %[c{i}]",
+                      f"ds_write_b64 %[k{i}], {self.reg(j)} ;@vfix 1" if write else f"ds_read_b64 %[x{i}], %[k{i}]"]
+            if not write:
+                L.append("s_waitcnt lgkmcnt(0)")
+                for i, j in enumerate(rows):
+                    L += [f"s_mov_b64 exec, %[c{i}]", f"v_mov_b64 {self.reg(j)}, %[x{i}] ;@vfix 0"]
+            L.append("s_mov_b64 exec, %[sv]")
+            outs = ['[sv] "=&s"(sv)'] + [f'[c{i}] "=&s"(c{i})' for i in range(4)] + [f'[k{i}] "=&v"(k{i})' for i in range(4)]
+            decl = "uint64_t sv, c0, c1, c2, c3;\n    uint32_t k0, k1, k2, k3;\n"
+            if not write:
+                outs += [f'[x{i}] "=&v"(x{i})' for i in range(4)]
+                decl += "    uint64_t x0, x1, x2, x3;\n"
+            ins = [f'[m{i}] "s"(m{i})' for i in range(4)] + [f'[ml{i}] "s"((uint32_t)m{i})' for i in range(4)] + \
+                  [f'[mh{i}] "s"((uint32_t)(m{i} >> 32))' for i in range(4)] + [f'[t{i}] "s"(t{i})' for i in range(4)] + \
+                  ['[ks] "s"(ks)', '[mb] "s"(mb)']
+            name = "w1src" if write else "w1tgt"
+            return (f"template <> __device__ __forceinline__ void {self.name}::{name}<{q}, {side}>(uint32_t ml, uint32_t mh, "
+                    f"uint32_t pre, uint32_t ks, uint32_t tl1, uint32_t mb) {{\n" + "\n".join(pro) + f"\n    {decl}"
+                    f"    asm volatile(\"{asm(L)}\"\n                 : {', '.join(outs)}\n                 : {', '.join(ins)}\n"
+                    f"                 : \"memory\", \"scc\");\n}}\n")
         L = ["s_nop 0"]  # (a VALU write of ml / mh / pre just before the block -> v_readlane of it: one wait state)
         for i, j in enumerate(rows):
             L += [f"v_readlane_b32 vcc_lo, %[ml], {j}", f"v_readlane_b32 vcc_hi, %[mh], {j}",
