@@ -1064,12 +1064,14 @@ struct VSel {
             // sources to the mailbox, then the kept side's targets take it (rows js..je: empty rows have no lanes)
             if (ks) {
                 const uint32_t tl1 = tL - 1u;
+                // L_k (k <= Ks) all lie below the cut and R_k (k <= Ks) at or above it: each side walks only its rows
+                const int jl = (int)((cut - 1u) >> 6), jr = (int)(cut >> 6);
                 if (right) {
-                    w1_ex<0, 0, true>(acc[0], acc[1], pkv, ks, tl1, mbb, js, je);
-                    w1_ex<0, 1, false>(acc[2], acc[3], pkv, ks, tl1, mbb, js, je);
+                    w1_ex<0, 0, true>(acc[0], acc[1], pkv, ks, tl1, mbb, js, jl);
+                    w1_ex<0, 1, false>(acc[2], acc[3], pkv, ks, tl1, mbb, jr, je);
                 } else {
-                    w1_ex<0, 1, true>(acc[2], acc[3], pkv, ks, tl1, mbb, js, je);
-                    w1_ex<0, 0, false>(acc[0], acc[1], pkv, ks, tl1, mbb, js, je);
+                    w1_ex<0, 1, true>(acc[2], acc[3], pkv, ks, tl1, mbb, jr, je);
+                    w1_ex<0, 0, false>(acc[0], acc[1], pkv, ks, tl1, mbb, js, jl);
                 }
             }
             if (tracing()) {  // (wave 0 only: no barrier; the record counter is wave 0's)
