@@ -211,6 +211,7 @@ __global__ void __launch_bounds__(kGradThreads) abs_grad_kernel(uint8_t* stacks,
 // measured slower on the same box.)
 constexpr int kL01Waves = 4;                  // independent waves per workgroup (strip x band each)
 constexpr int kL01Band = 32;                  // level-1 rows per band
+constexpr int kStripOwn = 61;                 // owner lanes per strip at most (lanes 0 and own + 1 <= 62 are halo)
 
 // (bound_ctrl: the lane without a source reads 0; no "old" operand to materialize)
 __device__ __forceinline__ uint32_t from_left(uint32_t v) {   // lane i <- lane i - 1 (wave_shr:1)
@@ -557,8 +558,11 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
     const int64_t npx = (int64_t)g.w[0] * g.h[0];
     int l = 1;
     if (g.levels >= 2 && pyr_mode() != 0) {
-        // strips of `own` lanes x 4 columns (<= 62 lanes: lanes 0 and 63 are halo), as few strips as the width needs
-        const int nstrip = (g.w[0] + 4 * 62 - 1) / (4 * 62);
+        // strips of `own` lanes x 4 columns, as few strips as the width needs.  own <= kStripOwn (61): lane 0 is the left
+        // halo, lane own + 1 the right halo, and the right halo's realigned dword takes its high bytes from lane own + 2
+        // (from_right), which must be a real lane; with own = 62 the halo lane 63 would read 0 from a lane 64 that does
+        // not exist and the last owner's level-1 gradient tap at the strip seam would be wrong.
+        const int nstrip = (g.w[0] + 4 * kStripOwn - 1) / (4 * kStripOwn);
         const int own = (g.w[0] + 4 * nstrip - 1) / (4 * nstrip);
         const int nband = (g.h[1] + kL01Band - 1) / kL01Band;
         const int waves = nstrip * nband;
@@ -567,7 +571,7 @@ void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t 
         l = 2;
         for (; l < g.levels; ++l) {
             const int w = g.w[l - 1];
-            const int ns = (w + 4 * 62 - 1) / (4 * 62);
+            const int ns = (w + 4 * kStripOwn - 1) / (4 * kStripOwn);
             const int ow = (w + 4 * ns - 1) / (4 * ns);
             const int band_rows = max(8, (g.h[l] + 7) / 8);  // bands of >= 8 output rows, ~8 waves per frame-stack
             const int nb = (g.h[l] + band_rows - 1) / band_rows;

@@ -32,7 +32,11 @@ def test_pyramid_bitexact():
     rng = np.random.default_rng(7)
     s = synth.make_pair()
     for (h, w, lv) in [(376, 1241, 5), (37, 101, 4), (64, 64, 3), (5, 7, 2), (3, 3, 2), (17, 300, 6), (300, 17, 6),
-                       (129, 4096, 3), (3, 9, 4), (4, 33, 5), (600, 900, 7), (95, 311, 4)]:
+                       (129, 4096, 3), (3, 9, 4), (4, 33, 5), (600, 900, 7), (95, 311, 4),
+                       # strip seams where 62 owner lanes would put the right halo on lane 63: odd widths
+                       # in (244n, 248n], and the own == 61 edge either side of them
+                       (40, 489, 3), (37, 739, 4), (20, 1239, 3), (21, 977, 3), (22, 991, 3), (18, 488, 3),
+                       (19, 245, 3), (23, 733, 5)]:
         imgs = [rng.integers(0, 256, (h, w), dtype=np.uint8) for _ in range(2)]
         if (h, w) == (376, 1241):
             imgs = [s.ref_img, s.cur_img] + imgs
