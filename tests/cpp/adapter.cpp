@@ -94,6 +94,53 @@ ImagePyramid::~ImagePyramid() {
 }
 // <<< ImagePyramid
 
+// >>> ImagePyramid getters
+// host copies on demand of the device stacks (the reference keeps cv::Mat stacks, src/image_pyramid.cpp:54-124).
+// Every svo_* return is checked: without a set, past the last level or on any failure a getter returns an empty Mat
+// (rows = cols = 0) and the sizes are (0, 0), as the reference's getImageSizeAtLevel past the last level.
+std::size_t ImagePyramid::getSizeImagePyramid() const {
+    std::size_t n = 0;
+    int32_t w = 0, h = 0;
+    while (m_set && svo_pyramid_level_size(m_set, (int32_t)n, &w, &h) == SVO_OK && w > 0) ++n;
+    return n;
+}
+cv::Size ImagePyramid::getImageSizeAtLevel(const std::size_t level) const {
+    int32_t w = 0, h = 0;
+    if (!m_set || level >= (std::size_t)INT32_MAX || svo_pyramid_level_size(m_set, (int32_t)level, &w, &h) != SVO_OK)
+        return cv::Size(0, 0);
+    return cv::Size(w, h);
+}
+cv::Size ImagePyramid::getBaseImageSize() const { return getImageSizeAtLevel(0); }
+const cv::Mat& ImagePyramid::hostLevel(const std::size_t level, const int32_t gradient) const {
+    const cv::Size sz = getImageSizeAtLevel(level);
+    m_none = cv::Mat();
+    if (sz.width == 0) return m_none;                                        // no set, or past the last level
+    std::vector<cv::Mat>& cache = gradient ? m_hostGradients : m_hostImages;
+    if (cache.size() <= level) cache.resize(level + 1);
+    cv::Mat& m = cache[level];
+    m.create(sz.height, sz.width, CV_8UC1);
+    if (svo_pyramid_set_download(m_set, 0, (int32_t)level, gradient, m.ptr<uint8_t>()) != SVO_OK) m = cv::Mat();
+    return m;
+}
+const cv::Mat& ImagePyramid::getImageAtLevel(const std::size_t level) const { return hostLevel(level, 0); }
+const cv::Mat& ImagePyramid::getGradientAtLevel(const std::size_t level) const { return hostLevel(level, 1); }
+const cv::Mat& ImagePyramid::getBaseImage() const { return hostLevel(0, 0); }
+const cv::Mat& ImagePyramid::getBaseGradientImage() const { return hostLevel(0, 1); }
+// the non-const overloads hand out the same host copy (writes to it do not reach the device stacks)
+cv::Mat& ImagePyramid::getImageAtLevel(const std::size_t level) {
+    return const_cast<cv::Mat&>(static_cast<const ImagePyramid&>(*this).getImageAtLevel(level));
+}
+cv::Mat& ImagePyramid::getGradientAtLevel(const std::size_t level) {
+    return const_cast<cv::Mat&>(static_cast<const ImagePyramid&>(*this).getGradientAtLevel(level));
+}
+const std::vector<cv::Mat>& ImagePyramid::getAllImages() const {
+    const std::size_t n = getSizeImagePyramid();
+    for (std::size_t l = 0; l < n; ++l) hostLevel(l, 0);
+    m_hostImages.resize(n);
+    return m_hostImages;
+}
+// <<< ImagePyramid getters
+
 // >>> FeatureAlignment::align
 double FeatureAlignment::align(const std::shared_ptr<Feature>& ref, const std::shared_ptr<Frame>& cur,
                                Eigen::Vector2d& pixelPos) {

@@ -8,7 +8,8 @@
 // int32 n_fa; double fa_ref_px[2 n_fa] fa_init[2 n_fa] (FeatureAlignment(7) from the ref frame into cur).
 // `fail` makes the adapter's context on a device index that does not exist first.
 // Output lines: "err <v>", "pose <7 values>", "unchanged <0|1>" (the pose bits after vs before), "again <0|1>"
-// (a second align from the same start gives the same bits), "fa <i> <x> <y> <err>".
+// (a second align from the same start gives the same bits), "fa <i> <x> <y> <err>", and the ref frame's pyramid
+// through the ImagePyramid getters ("pyr", "lvl", "all" lines, see below).
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -69,6 +70,28 @@ int main(int argc, char** argv) {
             ft->m_point->m_position = {pt[3 * i], pt[3 * i + 1], pt[3 * i + 2]};
         }
         ft->m_frame->m_features.push_back(ft);
+    }
+    // the pyramid getters (include/image_pyramid.hpp:75-140) on the ref frame, one level past the last included:
+    // "pyr <levels> <base w> <base h>", then per level "lvl <l> <w> <h> <rows> <cols> <fnv1a(image)> <fnv1a(gradient)>"
+    {
+        const ImagePyramid& pyr = ref->m_imagePyramid;
+        auto fnv = [](const cv::Mat& m) {
+            uint64_t x = 1469598103934665603ull;
+            for (uint8_t b : m.buf) x = (x ^ b) * 1099511628211ull;
+            return (unsigned long long)x;
+        };
+        const cv::Size b = pyr.getBaseImageSize();
+        std::printf("pyr %zu %d %d\n", pyr.getSizeImagePyramid(), b.width, b.height);
+        for (int32_t l = 0; l <= levels; ++l) {
+            const cv::Size sz = pyr.getImageSizeAtLevel((size_t)l);
+            const cv::Mat& im = pyr.getImageAtLevel((size_t)l);
+            const cv::Mat& gr = pyr.getGradientAtLevel((size_t)l);
+            std::printf("lvl %d %d %d %d %d %llu %llu\n", l, sz.width, sz.height, im.rows, im.cols, fnv(im), fnv(gr));
+        }
+        const std::vector<cv::Mat>& all = pyr.getAllImages();
+        const bool base_ok = fnv(pyr.getBaseImage()) == fnv(pyr.getImageAtLevel(0)) &&
+                             fnv(pyr.getBaseGradientImage()) == fnv(pyr.getGradientAtLevel(0));
+        std::printf("all %zu %d\n", all.size(), base_ok ? 1 : 0);
     }
     ImageAlignment ia((uint32_t)patch, minL, maxL, 6);
     const Sophus::SE3d before = cur->m_absPose;

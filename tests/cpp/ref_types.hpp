@@ -51,12 +51,27 @@ struct SE3d {
 }  // namespace Sophus
 
 namespace cv {
+constexpr int CV_8UC1 = 0;
+struct Size {  // cv::Size(width, height)
+    int width = 0, height = 0;
+    Size() = default;
+    Size(int w, int h) : width(w), height(h) {}
+};
 struct Mat {  // CV_8UC1, continuous
     int rows = 0, cols = 0;
     std::vector<uint8_t> buf;
     template <class T> const T* ptr() const { return reinterpret_cast<const T*>(buf.data()); }
+    template <class T> T* ptr() { return reinterpret_cast<T*>(buf.data()); }
+    void create(int r, int c, int /*type: CV_8UC1*/) {
+        rows = r;
+        cols = c;
+        buf.assign((size_t)r * (size_t)c, 0);
+    }
+    bool empty() const { return buf.empty(); }
+    Size size() const { return Size(cols, rows); }
 };
 }  // namespace cv
+using cv::CV_8UC1;
 
 class PinholeCamera {
 public:
@@ -80,9 +95,23 @@ public:
     ~ImagePyramid();
     void createImagePyramid(const cv::Mat& baseImage, std::size_t levels);
     svo_pyramid_set* set() const { return m_set; }
+    // the getters of include/image_pyramid.hpp:75-140 (const forms; the adapter adds the non-const ones)
+    const std::vector<cv::Mat>& getAllImages() const;
+    const cv::Mat& getImageAtLevel(std::size_t level) const;
+    cv::Mat& getImageAtLevel(std::size_t level);
+    const cv::Mat& getBaseImage() const;
+    const cv::Mat& getBaseGradientImage() const;
+    const cv::Mat& getGradientAtLevel(std::size_t level) const;
+    cv::Mat& getGradientAtLevel(std::size_t level);
+    std::size_t getSizeImagePyramid() const;
+    cv::Size getImageSizeAtLevel(std::size_t level) const;
+    cv::Size getBaseImageSize() const;
 
 private:
+    const cv::Mat& hostLevel(std::size_t level, int32_t gradient) const;
     svo_pyramid_set* m_set = nullptr;  // the adapter's member: the frame's device-resident stacks
+    mutable std::vector<cv::Mat> m_hostImages, m_hostGradients;  // host copies the getters fill on demand
+    mutable cv::Mat m_none;                                        // what a getter returns on failure (empty)
 };
 
 class Frame;

@@ -1,8 +1,10 @@
 """BASELINE config 4 (512 synthetic frame pairs, independent, sharded over GPUs with no collective) and the
 robust-scale kernel choice.
 
-* the headline batch shape: one 512-pair reference-mode batch (two 256-pair K2V chains) over 16 distinct scenes,
+* the headline batch shape: one 512-pair reference-mode batch (four 128-pair K2V chains) over 16 distinct scenes,
   every pair against the oracle's std::nth_element path and bit for bit against a single-pair run of its scene;
+* config 4 as SURVEY 8(d) defines it: 512 pairs on 512 distinct scenes (seeds 0x5EED0000 + pair), every pair against
+  the oracle;
 * the N > 1 rank path on the GPU: bench.py --gpus 2 (both ranks on device 0, SVO_BENCH_SHARED_GPU=1) dumps every
   pair's pose; a --gpus 1 run over the same 2 x P pairs (--scene-block P) must give the same bits (SURVEY §8(e):
   per-pair outputs independent of the number of ranks);
@@ -91,7 +93,7 @@ def test_gpu_config4_batch_512_pairs():
     b.set_pairs(0, ps, ps, ps, *_packed(sc, range(P)))
     b.run()
     poses, err, st = b.results()
-    for i in (0, 255, 256, 511):  # both 256-pair chains ran K2V at every level
+    for i in (0, 127, 128, 255, 256, 383, 384, 511):  # every 128-pair chain (capi.hip kSplitsRefv) ran K2V at every level
         assert [b.traces(i)[l].scale_kernel for l in range(L)] == [svo_amd.SCALE_K2V] * L, i
     ref = [oracle_align(s, PATCH, 0, L - 1, mode=0, trace=False) for s in sc]
     for i in range(P):
@@ -104,6 +106,41 @@ def test_gpu_config4_batch_512_pairs():
         for i in range(d, P, D):
             assert np.array_equal(p1[0], poses[i]) and e1[0] == err[i] and s1[0] == st[i], (d, i)
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_gpu_config4_512_distinct_scenes():
+    """SURVEY 8(d) config 4 as defined: 512 pairs, pair p on the scene seeded 0x5EED0000 + p (no repeated scene), in
+    the bench's detector cell order; every pair against the oracle's std::nth_element path (VERDICT r5 item 4).  The
+    scenes and the oracle run on a host thread pool (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    ctx = svo_amd.default_context()
+    P, NF = 512, 2000
+    workers = max(1, min(16, os.cpu_count() or 1))
+    with ThreadPoolExecutor(workers) as ex:
+        sc = list(ex.map(lambda p: synth.make_pair(seed=synth.SEED_BASE + p, n_features=NF, patch_size=PATCH, nthreads=1,
+                                                   cell_order=30), range(P)))
+    print(f"512 scenes generated on {workers} threads", flush=True)
+    ps = _pyramids(sc, ctx)
+    cam = _camera(sc[0])
+    b = svo_amd.AlignBatch(cam, PATCH, 0, L - 1, P, NF, ctx, median_mode=svo_amd.MEDIAN_REFERENCE)
+    b.set_pairs(0, ps, ps, ps, *_packed(sc, range(P)))
+    b.run()
+    poses, err, st = b.results()
+    for i in (0, 127, 128, 255, 256, 383, 384, 511):
+        assert [b.traces(i)[l].scale_kernel for l in range(L)] == [svo_amd.SCALE_K2V] * L, i
+    b.run()  # a second run of the same batch: the same bits
+    p2, e2, s2 = b.results()
+    assert np.array_equal(p2, poses) and np.array_equal(e2, err) and np.array_equal(s2, st)
+    b.close()
+    with ThreadPoolExecutor(workers) as ex:
+        ref = list(ex.map(lambda s: oracle_align(s, PATCH, 0, L - 1, mode=0, trace=False)[:3], sc))
+    for i in range(P):
+        pc, ec, stc = ref[i]
+        assert st[i] == stc, i
+        assert np.abs(canon(poses[i]) - canon(pc)).max() <= 1e-9, i
+        assert abs(err[i] - ec) <= 1e-9 * max(ec, 1e-300), i
 
 
 def _run_bench(args, out, env_extra):

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box runner: each GPU step under its own time limit; stops at the first crash/timeout
 # (exit >= 124), continues past ordinary test failures so the later measurements still run.
-# usage: tools/gpu_round.sh <step>...   steps: smoke tests bench prof pmc
+# usage: tools/gpu_round.sh <step>...   steps: smoke quick tests bench prof hprof d512 pmc
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -24,6 +24,11 @@ for step in "$@"; do
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu
               # the longest dispatches of the same trace, committed beside every kernel-stats summary
               python3 tools/top_dispatches.py gpurun_out/prof/run_kernel_trace.csv 10 > gpurun_out/top_dispatches.txt && cat gpurun_out/top_dispatches.txt ;;
+        # the headline alone (no secondary / batch-scaling / latency lines), its kernel trace split by launch shape
+        hprof) run hprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/hprof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu --no-secondary --core-only
+               python3 tools/headline_kernel_stats.py gpurun_out/hprof/run_kernel_trace.csv > gpurun_out/headline_kernel_stats.csv && cat gpurun_out/headline_kernel_stats.csv ;;
+        # config 4's 512 distinct scenes (seeds 0x5EED0000 + pair), the timed loop only
+        d512) run d512 600 python3 bench.py --distinct 512 --no-cpu --no-secondary --core-only ;;
         pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-secondary --core-only
              run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu --no-secondary --core-only
              python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > gpurun_out/pmc_traffic.json && cat gpurun_out/pmc_traffic.json ;;
