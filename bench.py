@@ -6,7 +6,9 @@ frame pairs, 1241x376 grey, 2000 features (1000 on the ref frame + 1000 on its l
 5-level pyramid (levels 4..0), one Tukey-weighted LM step per level.  A "step" is one pass of the hot
 path over one batch: --pairs independent pairs per GPU (default 512), inputs (pyramids, features,
 poses) resident in HBM before the timed region.  Data: synthetic street scenes (svo_amd.synth, seeds
-0x5EED0000 + global pair index modulo --distinct), each pair in its own HBM buffers.
+0x5EED0000 + global pair index, SURVEY.md §8(d): every pair its own scene; --distinct D repeats D scenes instead),
+each pair in its own HBM buffers.  The line also times the round 1-5 workload (16 scenes repeated) on the same batch
+(`workload_16_distinct_scenes`).
 
 Multi-GPU: one process per GPU; pairs are independent, so each rank aligns its own --pairs (weak
 scaling) and there is no data-path collective: the gloo process group is used only for the barrier and
@@ -46,7 +48,8 @@ def parse():
     ap.add_argument("--features", type=int, default=2000)
     ap.add_argument("--levels", type=int, default=5)
     ap.add_argument("--patch", type=int, default=5)
-    ap.add_argument("--distinct", type=int, default=16, help="distinct synthetic scenes per scene block")
+    ap.add_argument("--distinct", type=int, default=0,
+                    help="distinct synthetic scenes per scene block (0: every pair its own scene, SURVEY 8(d))")
     ap.add_argument("--scene-block", type=int, default=0,
                     help="global pair g uses the scene seeded SEED_BASE + (g // B) * B + (g % B) %% distinct, B = this "
                          "value (default: --pairs, i.e. each rank's own block): the job's pairs are then the same "
@@ -171,15 +174,17 @@ def main():
     shared_gpu = os.environ.get("SVO_BENCH_SHARED_GPU") == "1"
     ctx = svo_amd.Context(0 if shared_gpu else local_rank)
     P, nf, L, patch = args.pairs, args.features, args.levels, args.patch
-    D = max(1, min(args.distinct, P))
+    D = P if args.distinct <= 0 else max(1, min(args.distinct, P))
     nthreads = max(1, min(16, os.cpu_count() or 1))
     first, _ = shard.pair_block(world * P, rank, world)  # this rank's block of the job's world * P pairs
     cell = 30 if args.feature_order == "cell" else 0  # config "cell_pixel_size": 30
     seeds = scene_seeds(first, P, args.scene_block or P, D)
     useeds = sorted(set(seeds))
     sidx = [useeds.index(s) for s in seeds]  # pair j -> its scene in `scenes`
-    scenes = [synth.make_pair(seed=sd, n_features=nf, patch_size=patch, nthreads=nthreads, cell_order=cell)
-              for sd in useeds]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(nthreads) as ex:  # (ctypes releases the GIL: one scene per host thread)
+        scenes = list(ex.map(lambda sd: synth.make_pair(seed=sd, n_features=nf, patch_size=patch, nthreads=1,
+                                                         cell_order=cell), useeds))
     cam = scenes[0].camera
     camera = svo_amd.PinholeCamera(cam["width"], cam["height"], cam["fx"], cam["fy"], cam["cx"], cam["cy"])
     rep = [sidx.index(k) for k in range(len(scenes))]  # the first pair of each scene
@@ -252,6 +257,28 @@ def main():
         step_s.append(time.perf_counter() - t)
     step_med = float(np.median(step_s))
     stages = batch.profile()  # one extra, event-instrumented run (outside the timed region)
+    # the round 1-5 headline workload on the same batch and pyramids: pair i on scene i % 16 (SEED_BASE + i % 16, the
+    # first 16 scenes of this set when every pair has its own scene); timed like the headline; not `value`
+    w16 = None
+    if D == P and P >= 16 and args.scene_block in (0, P):
+        idx16 = [i % 16 for i in range(P)]
+        pk16 = list(packed_pairs(scenes, P, 16, [sidx[k] for k in idx16]))
+        pk16[0] = np.array([[3 * k, 3 * k + 1, 3 * k + 2] for k in idx16], np.int32)  # frames of scene i % 16
+        batch.set_pairs(0, ps, ps, ps, *pk16)
+        for _ in range(2):
+            batch.run()
+        ctx.synchronize()
+        t16 = time.perf_counter()
+        for _ in range(args.steps):
+            batch.run()
+        ctx.synchronize()
+        dt16 = (time.perf_counter() - t16) / args.steps
+        p16, _, _ = batch.results()
+        w16 = {"pairs_per_s": round(P / dt16, 1), "ms_per_step": round(dt16 * 1e3, 4), "distinct_scenes": 16,
+               "poses_equal_their_scene": bool(all(np.array_equal(p16[i], poses[i % 16]) for i in range(P))),
+               "note": "rounds 1-5 headline workload: pair i on scene SEED_BASE + i % 16 (each scene 32 times); "
+                       "same batch, pyramids and timing as the headline"}
+        batch.set_pairs(0, ps, ps, ps, *packed)  # (back on the headline's pairs)
     # end to end from host memory (outside the timed region; never `value`): upload the 3P base images,
     # build the pyramids, hand over every pair's features and poses, align, read the results back
     ctx.synchronize()
@@ -425,6 +452,12 @@ def main():
                     "while batch i aligns; then batch i's results come back and batch i+1 is queued"},
         "latency": lat,
         "batch_scaling": scaling_lines,
+        "workload_16_distinct_scenes": w16,
+        # key meanings across rounds: end_to_end_device_images is one batch at a time in rounds 1-3 and 5-6
+        # (round 4 alone reported the pipelined stream under it, now end_to_end_device_images_pipelined); the headline
+        # runs every pair on its own scene from round 6 (16 repeated scenes in rounds 1-5: workload_16_distinct_scenes)
+        "schema": {"round": 6, "end_to_end_device_images": "one batch at a time (rounds 1-3, 5-6)",
+                   "headline_scenes": "one scene per pair (round 6); 16 repeated scenes (rounds 1-5)"},
     }
     if not args.no_secondary:
         out["secondary"] = secondary(args, ctx, scenes[0], cam, camera)
@@ -823,13 +856,14 @@ def cpu_baseline(args, scenes, gpu_poses, L, patch, nthreads, mode=None):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # noqa: E402  (CPU baseline / checker only)
     omode = 1 if mode == svo_amd.MEDIAN_EXACT else 0  # oracle median_mode 0 = the reference's nth_element
-    pyrs = [[O.build_pyramid(im, L)[0] for im in (s.ref_img, s.kf_img, s.cur_img)] for s in scenes]
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(nthreads)  # (the checker's pyramids and poses; ctypes releases the GIL)
+    pyrs = list(pool.map(lambda s: [O.build_pyramid(im, L)[0] for im in (s.ref_img, s.kf_img, s.cur_img)], scenes))
     pairs = [O.make_pair(p[0], p[1], p[2], s.ref_pose, s.kf_pose, s.n_ref, s.n_kf, s.px, s.bearing, s.point, s.has_point)
              for p, s in zip(pyrs, scenes)]
-    se3_err = 0.0
-    for i, s in enumerate(scenes):
-        pose, _, _, _ = O.image_align(s.camera, patch, 0, L - 1, pairs[i], s.cur_init_pose, omode)
-        se3_err = max(se3_err, float(np.abs(canon(pose) - canon(gpu_poses[i])).max()))
+    ref_poses = list(pool.map(lambda i: O.image_align(scenes[i].camera, patch, 0, L - 1, pairs[i],
+                                                      scenes[i].cur_init_pose, omode)[0], range(len(scenes))))
+    se3_err = max(float(np.abs(canon(ref_poses[i]) - canon(gpu_poses[i])).max()) for i in range(len(scenes)))
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     share = int(os.environ.get("OMP_NUM_THREADS", avail) or avail)
     threads = max(1, min(avail, share))
@@ -860,11 +894,10 @@ def cpu_baseline(args, scenes, gpu_poses, L, patch, nthreads, mode=None):
     nat_diff = None
     if nat is not None:
         nat_single, nat_multi = timed(nat)
-        nat_diff = max(float(np.abs(canon(O.image_align(s.camera, patch, 0, L - 1, pairs[i], s.cur_init_pose, omode,
-                                                           L=nat)[0])
-                                    - canon(O.image_align(s.camera, patch, 0, L - 1, pairs[i], s.cur_init_pose,
-                                                          omode)[0])).max())
-                       for i, s in enumerate(scenes))
+        nat_poses = list(pool.map(lambda i: O.image_align(scenes[i].camera, patch, 0, L - 1, pairs[i],
+                                                          scenes[i].cur_init_pose, omode, L=nat)[0], range(len(scenes))))
+        nat_diff = max(float(np.abs(canon(nat_poses[i]) - canon(ref_poses[i])).max()) for i in range(len(scenes)))
+    pool.shutdown()
     single, multi = (nat_single, nat_multi) if nat is not None else (port_single, port_multi)
     build = ("oracle/svo_oracle.cpp, -O3 -DNDEBUG -march=native (built on this host at bench time, FMA contraction "
              "allowed)" if nat is not None else

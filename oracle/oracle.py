@@ -222,6 +222,21 @@ def image_align(cam, patch, min_level, max_level, pair, cur_pose, median_mode=0,
     return pose, err, st.value, traces
 
 
+def image_align_vectors(cam, patch, min_level, max_level, pair, cur_pose, median_mode=0):
+    """image_align that also returns every level's residual vector (coarsest first) and its n_valid: the vectors the
+    reference's computeMedian / computeMAD run on (tools/k2v_round_table.py)."""
+    pose = np.ascontiguousarray(cur_pose, dtype=np.float64).copy()
+    st = ctypes.c_int32()
+    M = (pair.pair.n_ref + pair.pair.n_kf) * patch * patch
+    out = np.zeros(M * (max_level - min_level + 1))
+    nv = np.zeros(max_level - min_level + 1, np.uint32)
+    f = lib().oracle_image_align_vectors
+    f.restype = ctypes.c_int32
+    n = f(ctypes.byref(camera(cam)), patch, min_level, max_level, median_mode, ctypes.byref(pair.pair), _p(pose),
+          ctypes.byref(st), _p(out), ctypes.c_int64(len(out)), nv.ctypes.data_as(ctypes.c_void_p))
+    return [out[i * M:(i + 1) * M] for i in range(n)], [int(x) for x in nv[:n]]
+
+
 def image_align_batch(cam, patch, min_level, max_level, pairs, cur_poses, median_mode=0, nthreads=1, L=None):
     n = len(pairs)
     arr = (OcPair * n)(*[p.pair for p in pairs])

@@ -340,6 +340,13 @@ struct LevelTrace {  // per-level debug record (mirrors svo_level_debug in inclu
     double H[36], g[6], dx[6];
 };
 
+// test infrastructure: when set (oracle_image_align_vectors), each level's tukey_weighting appends the residual vector it
+// sees (the reference's feature-major slots, DBL_MAX for an invisible slot) and its n_valid
+static thread_local double* g_vec_dump = nullptr;
+static thread_local int64_t g_vec_cap = 0, g_vec_used = 0;
+static thread_local uint32_t* g_vec_nvalid = nullptr;
+static thread_local int32_t g_vec_levels = 0;
+
 struct Optimizer {
     int nu;                       // number of unknowns
     int median_mode = 0;
@@ -362,6 +369,11 @@ struct Optimizer {
         std::fill(vis.begin(), vis.end(), 0);
     }
     void tukey_weighting(uint32_t n_valid) {  // :485-514
+        if (g_vec_dump && g_vec_used + (int64_t)r.size() <= g_vec_cap) {
+            std::memcpy(g_vec_dump + g_vec_used, r.data(), r.size() * sizeof(double));
+            g_vec_used += (int64_t)r.size();
+            g_vec_nvalid[g_vec_levels++] = n_valid;
+        }
         double med = 0.0;
         const double mad = compute_mad(r, n_valid, median_mode, &med);
         double sigma = 1.482602218505602 * mad;
@@ -1049,6 +1061,22 @@ double oracle_image_align(const oc_camera* c, int32_t patch, int32_t min_level, 
 }
 
 int32_t oracle_level_trace_size(void) { return (int32_t)sizeof(LevelTrace); }
+
+// oracle_image_align that also returns the residual vector of every level's robust scale, coarsest level first,
+// back to back in `out` (cap doubles) with each level's n_valid in nvalid_out; returns the number of levels stored
+// (tools/k2v_round_table.py: the block rounds of the reference's nth_element on real config-2 vectors)
+int32_t oracle_image_align_vectors(const oc_camera* c, int32_t patch, int32_t min_level, int32_t max_level,
+                                   int32_t median_mode, const oc_pair* P, double* cur_pose_inout, int32_t* status_out,
+                                   double* out, int64_t cap, uint32_t* nvalid_out) {
+    g_vec_dump = out;
+    g_vec_cap = cap;
+    g_vec_used = 0;
+    g_vec_nvalid = nvalid_out;
+    g_vec_levels = 0;
+    oracle_image_align(c, patch, min_level, max_level, median_mode, P, cur_pose_inout, status_out, nullptr);
+    g_vec_dump = nullptr;
+    return g_vec_levels;
+}
 
 // ImageAlignment::computeImageJac (src/image_alignment.cpp:194-248): out = 2 x 6 row-major
 void oracle_image_jac(const double* p3, double fx, double fy, double* out12) {

@@ -260,6 +260,25 @@ class Point:
         except Exception:  # (interpreter shutdown)
             pass
 
+    # copies own a fresh row: copying _i would alias one row between two Points and put it on the free list twice
+    # 
+    def _state(self):
+        i = self._i
+        return (_PT.pos[i].copy(), int(_PT.type[i]), int(_PT.last[i]), int(_PT.succ[i]), int(_PT.fail[i]))
+
+    def __copy__(self):
+        return _point_from_state(self._state(), self.features)
+
+    def __deepcopy__(self, memo):
+        import copy
+        p = _point_from_state(self._state(), ())
+        memo[id(self)] = p
+        p.features = copy.deepcopy(self.features, memo)
+        return p
+
+    def __reduce__(self):
+        return (_point_from_state, (self._state(), self.features))
+
     type = property(lambda self: int(_PT.type[self._i]), lambda self, v: _PT.type.__setitem__(self._i, v))
     last_projected_kf_id = property(lambda self: int(_PT.last[self._i]),
                                     lambda self, v: _PT.last.__setitem__(self._i, v))
@@ -286,6 +305,15 @@ class Point:
     def position(self, v):
         _PT.pos[self._i] = np.asarray(v, np.float64).reshape(3)
         Point._ver += 1
+
+
+def _point_from_state(state, features):
+    """A Point on a row of its own holding `state` (Point._state()) and observed by `features` (copy / pickle)."""
+    p = Point(state[0])
+    i = p._i
+    _PT.type[i], _PT.last[i], _PT.succ[i], _PT.fail[i] = state[1:]
+    p.features = list(features)
+    return p
 
 
 class Feature:

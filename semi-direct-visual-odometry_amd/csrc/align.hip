@@ -32,6 +32,11 @@
 #include "svo_wave.h"
 
 namespace svo {
+#if defined(SVO_TIMELINE)
+SVO_TL_DEFINE(k13)
+SVO_TL_READER(k13)
+#endif
+
 
 namespace {
 
@@ -283,6 +288,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 3 : 2) align_residual
     // 200-B lane stride touched 64 lines per instruction)
     constexpr bool kLds = G::A * kLaneFeats * (int)sizeof(KeyT) <= (kRef ? 65536 : 32768);
     __shared__ __attribute__((aligned(16))) KeyT kbuf[kLds ? G::A * kLaneFeats : 1];
+    SVO_TL_SCOPE(k13, kTlK1, level, a.pair_base);
     int pair, chunk;
     xcd_pair_chunk(a.chunks, pair, chunk);
     if (pair >= a.n_pairs) return;
@@ -1214,6 +1220,7 @@ __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_
     __shared__ SolveShared ssh;
     __shared__ double part[kLaneWaves][28];
     __shared__ uint32_t last_flag;
+    SVO_TL_SCOPE(k13, kTlK3, level, a.pair_base);
     int pair, chunk;
     xcd_pair_chunk(a.chunks, pair, chunk);
     if (pair >= a.n_pairs) return;

@@ -39,6 +39,11 @@
 #include <utility>
 
 namespace svo {
+#if defined(SVO_TIMELINE)
+SVO_TL_DEFINE(k2v)
+SVO_TL_READER(k2v)
+#endif
+
 
 namespace {
 
@@ -1333,6 +1338,7 @@ template <class L>
 __global__ void __launch_bounds__(kVT, 1) align_scale_refv_kernel(AlignArgs a, int level) {
     __shared__ VShared<L> sh;
     (void)level;
+    SVO_TL_SCOPE(k2v, kTlK2V, level, a.pair_base);
     scale_refv_pair<L>(a, sh);
 }
 template __global__ void align_scale_refv_kernel<LayA>(AlignArgs, int);

@@ -95,6 +95,57 @@ int align_win_dwords(int half);                         // window dwords per fea
 int align_chunks(int max_f, int half, int feat_iters);  // K1/K3 workgroups per pair
 void launch_pyramid(uint8_t* stacks, const LevelGeom& g, int32_t first, int32_t count, hipStream_t s);
 
+#if defined(SVO_TIMELINE)
+// Diagnostic build only (make timeline -> build/timeline/): one record per workgroup of K1 / K2V / K3 with its start
+// and end on the chip-wide 100 MHz clock and the CU it ran on, so a step's CU time can be split by kernel and idle
+// (tools/timeline.py).  A TlScope at the top of a kernel body records the workgroup when it goes out of scope, early
+// returns included; thread 0's clock stands for the workgroup.
+struct TlRec {
+    uint64_t t0, t1;
+    uint32_t kind, level, block, hw, xcc, pair_base;
+};
+constexpr uint32_t kTlCap = 1u << 18;
+enum : uint32_t { kTlK1 = 1, kTlK2V = 2, kTlK3 = 3 };
+struct TlScope {
+    TlRec* rec;
+    uint32_t* n;
+    uint64_t t0;
+    uint32_t kind, level, pb;
+    __device__ __forceinline__ TlScope(TlRec* r, uint32_t* nn, uint32_t k, uint32_t l, uint32_t p)
+        : rec(r), n(nn), t0(__builtin_amdgcn_s_memrealtime()), kind(k), level(l), pb(p) {}
+    __device__ __forceinline__ ~TlScope() {
+        if (threadIdx.x == 0) {
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave, SIMD, CU, SH, SE
+            const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+            const uint32_t i = __hip_atomic_fetch_add(n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (i < kTlCap) rec[i] = TlRec{t0, t1, kind, level, blockIdx.x, hw, xcc, pb};
+        }
+    }
+};
+#define SVO_TL_DEFINE(tag)                    \
+    __device__ TlRec g_tl_rec_##tag[kTlCap]; \
+    __device__ uint32_t g_tl_n_##tag;
+#define SVO_TL_SCOPE(tag, kind, level, pb) TlScope tl_scope_(g_tl_rec_##tag, &g_tl_n_##tag, kind, (uint32_t)(level), (uint32_t)(pb))
+// extern "C" int svo_debug_timeline_<tag>(void* out, size_t bytes, uint32_t* count, int reset): copy the records out
+// (or, with reset, zero the count)
+#define SVO_TL_READER(tag)                                                                                       \
+    extern "C" int svo_debug_timeline_##tag(void* out, size_t bytes, uint32_t* count, int reset) {                \
+        if (reset) {                                                                                             \
+            const uint32_t z = 0;                                                                                \
+            return hipMemcpyToSymbol(HIP_SYMBOL(g_tl_n_##tag), &z, sizeof z) == hipSuccess ? 0 : -2;             \
+        }                                                                                                        \
+        if (hipMemcpyFromSymbol(count, HIP_SYMBOL(g_tl_n_##tag), sizeof(uint32_t)) != hipSuccess) return -2;     \
+        const size_t want = (size_t)(*count < kTlCap ? *count : kTlCap) * sizeof(TlRec);                         \
+        return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tl_rec_##tag), bytes < want ? bytes : want) == hipSuccess ? 0 \
+                                                                                                               : -2; \
+    }
+#else
+#define SVO_TL_SCOPE(tag, kind, level, pb) \
+    do {                                   \
+    } while (0)
+#endif
+
 struct FeatureAlignArgs {
     const uint8_t* const* ref_grad;  // [n] level-0 gradient image of each candidate's reference frame
     const uint8_t* cur_grad;         // level-0 gradient image of the current frame

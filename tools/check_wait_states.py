@@ -1,4 +1,9 @@
-"""Build-time check of the wait states K2V's inline-asm blocks depend on.
+"""Build-time check of five gfx9 wait-state rules (R1-R5 below) around K2V's inline-asm blocks.
+
+Scope: only the five rules listed below are modelled.  Hazards outside them -- among others the gfx940 / gfx950 rules
+for a VALU write of EXEC followed by v_readlane / v_writelane, the s_set_gpr_idx_on / s_set_gpr_idx_off mode
+switches, and transcendental-op forwarding -- are not checked, so a clean pass means "no R1-R5 violation", not
+"hazard-free" (ADVICE r5).
 
 hipcc inserts the wait states gfx9 needs between its own instructions, but nothing inside an inline-asm block, and
 an asm block's first instructions may follow a compiler instruction that needs them (round 4's GPU fault: a
