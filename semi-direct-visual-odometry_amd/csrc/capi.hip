@@ -64,9 +64,17 @@ constexpr int32_t kSplitsRefvMin = 512;
 
 struct svo_ctx {
     int32_t device;
-    hipStream_t stream;
+    // the context stream; every use goes through ctx_stream(), which first joins a batch's pending chains (below)
+    hipStream_t stream_raw;
     hipStream_t sides[4];         // extra streams: a batch runs as concurrent sub-batch chains
     hipEvent_t fork, joins[4];    // sides wait for stream at fork; stream waits for each side at its join
+    // Chains of a batch run are joined into the context stream lazily: a run leaves its side chains pending, the
+    // next run of the same batch (same split) lets each chain follow its own previous run on its own stream, and any
+    // other use of the context stream joins them first (ctx_stream).  So back-to-back runs of one batch are ordered
+    // per chain -- the only data dependency between them: chain i reads and writes only its own pairs -- instead of
+    // every chain of run k + 1 waiting for the slowest chain of run k.  SVO_DEFER_JOIN=0 joins after every run.
+    const struct svo_align_batch* pending_batch = nullptr;
+    int pending_chains = 0;
     hipEvent_t chain_marks[3][2 + 3 * svo::kMaxLevels];  // launch marks of chains 0..2 (staggered starts)
     hipEvent_t events[16];
     // svo_align_batch_set_pairs uploads on its own stream, so the copies overlap a pyramid build queued
@@ -93,6 +101,22 @@ struct svo_ctx {
     // batches' runs join the sets their pairs read from this list (a batch never dereferences a set it keeps)
     std::vector<svo_pyramid_set*> pending_sets;
 };
+
+// the context stream after the pending chains of the last batch run (see svo_ctx::pending_batch)
+static hipStream_t ctx_stream(svo_ctx* c) {
+    if (c->pending_batch) {
+        for (int i = 1; i < c->pending_chains; ++i) {
+            const hipError_t e = hipStreamWaitEvent(c->stream_raw, c->joins[i], 0);
+            if (e != hipSuccess) {  // (valid handles: not expected) fall back to a full wait so nothing overlaps
+                (void)hipStreamSynchronize(c->sides[i]);
+                (void)hipGetLastError();
+            }
+        }
+        c->pending_batch = nullptr;
+        c->pending_chains = 0;
+    }
+    return c->stream_raw;
+}
 
 // at least `bytes` of the context's scratch (the previous contents are not kept)
 static hipError_t ctx_scratch(svo_ctx* c, size_t bytes, void** out) {
@@ -129,7 +153,7 @@ static hipError_t ctx_pinned_alloc(svo_ctx* c) {
 
 static hipError_t ctx_ring_drain(svo_ctx* c) {
     if (!c->ring_pending) return hipSuccess;
-    const hipError_t e = hipStreamSynchronize(c->stream);
+    const hipError_t e = hipStreamSynchronize(ctx_stream(c));
     c->ring_pending = false;
     c->ring_off = 0;
     return e;
@@ -207,7 +231,7 @@ static hipError_t set_join(const svo_pyramid_set* cp) {
     p->pending = false;
     pending_remove(p->ctx, p);
     hipError_t e = hipSetDevice(p->ctx->device);
-    if (e == hipSuccess) e = hipStreamWaitEvent(p->ctx->stream, p->ready, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx_stream(p->ctx), p->ready, 0);
     return e;
 }
 // the sets among `sets` that still have a pending asynchronous build (matched by address against the context's
@@ -287,7 +311,7 @@ int svo_ctx_create(int32_t device, svo_ctx** out) {
     svo_ctx* c = new (std::nothrow) svo_ctx{};
     if (!c) return fail(SVO_ERR_ARG, "out of host memory");
     c->device = device;
-    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    hipError_t e = hipStreamCreateWithFlags(&c->stream_raw, hipStreamNonBlocking);
     for (int i = 1; i < 4 && e == hipSuccess; ++i) e = hipStreamCreateWithFlags(&c->sides[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->prep, hipStreamNonBlocking);
@@ -311,7 +335,7 @@ int svo_ctx_create(int32_t device, svo_ctx** out) {
 int svo_ctx_destroy(svo_ctx* c) {
     if (!c) return SVO_OK;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(ctx_stream(c));
     for (hipEvent_t ev : c->events)
         if (ev) (void)hipEventDestroy(ev);
     if (c->copy) (void)hipStreamSynchronize(c->copy);
@@ -331,7 +355,7 @@ int svo_ctx_destroy(svo_ctx* c) {
     }
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->pinned) (void)hipHostFree(c->pinned);
-    (void)hipStreamDestroy(c->stream);
+    (void)hipStreamDestroy(c->stream_raw);
     delete c;
     return SVO_OK;
 }
@@ -339,16 +363,16 @@ int svo_ctx_destroy(svo_ctx* c) {
 int svo_ctx_synchronize(svo_ctx* c) {
     if (!c) return fail(SVO_ERR_ARG, "ctx is null");
     SVO_HIP(hipSetDevice(c->device));
-    SVO_HIP(hipStreamSynchronize(c->stream));
+    SVO_HIP(hipStreamSynchronize(ctx_stream(c)));
     return SVO_OK;
 }
 
-void* svo_ctx_stream(svo_ctx* c) { return c ? (void*)c->stream : nullptr; }
+void* svo_ctx_stream(svo_ctx* c) { return c ? (void*)ctx_stream(c) : nullptr; }
 
 int svo_ctx_event_record(svo_ctx* c, int32_t slot) {
     if (!c || slot < 0 || slot >= 16) return fail(SVO_ERR_ARG, "bad context or event slot");
     SVO_HIP(hipSetDevice(c->device));
-    SVO_HIP(hipEventRecord(c->events[slot], c->stream));
+    SVO_HIP(hipEventRecord(c->events[slot], ctx_stream(c)));
     return SVO_OK;
 }
 
@@ -389,7 +413,7 @@ int svo_pyramid_set_create(svo_ctx* c, int32_t n_frames, int32_t width, int32_t 
 int svo_pyramid_set_destroy(svo_pyramid_set* p) {
     if (!p) return SVO_OK;
     (void)hipSetDevice(p->ctx->device);
-    (void)hipStreamSynchronize(p->ctx->stream);
+    (void)hipStreamSynchronize(ctx_stream(p->ctx));
     if (p->ready) {
         (void)hipStreamSynchronize(p->ctx->prep);
         (void)hipEventDestroy(p->ready);
@@ -407,7 +431,7 @@ static int upload_impl(svo_pyramid_set* p, int32_t first, int32_t count, const u
     SVO_HIP(set_join(p));
     const size_t img = (size_t)p->width * p->height;
     SVO_HIP(hipMemcpy2DAsync(p->d_base + (size_t)first * p->stride, (size_t)p->stride, src, img, img, count, kind,
-                             p->ctx->stream));
+                             ctx_stream(p->ctx)));
     return SVO_OK;
 }
 
@@ -425,7 +449,7 @@ int svo_pyramid_set_build(svo_pyramid_set* p, int32_t first, int32_t count) {
     if (count == 0) return SVO_OK;
     SVO_HIP(hipSetDevice(p->ctx->device));
     SVO_HIP(set_join(p));
-    svo::launch_pyramid(p->d_base, p->geom, first, count, p->ctx->stream);
+    svo::launch_pyramid(p->d_base, p->geom, first, count, ctx_stream(p->ctx));
     SVO_HIP(hipGetLastError());
     return SVO_OK;
 }
@@ -439,7 +463,7 @@ int svo_pyramid_set_build_async(svo_pyramid_set* p, int32_t first, int32_t count
     if (!p->ready) SVO_HIP(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
     // after everything the context stream holds now (the uploads of these frames, and the alignment that
     // last read the planes), and after an earlier asynchronous build of this set (the prep stream is in order)
-    SVO_HIP(hipEventRecord(c->prep_gate, c->stream));
+    SVO_HIP(hipEventRecord(c->prep_gate, ctx_stream(c)));
     SVO_HIP(hipStreamWaitEvent(c->prep, c->prep_gate, 0));
     svo::launch_pyramid(p->d_base, p->geom, first, count, c->prep);
     SVO_HIP(hipGetLastError());
@@ -455,8 +479,8 @@ int svo_pyramid_set_download(const svo_pyramid_set* p, int32_t frame, int32_t le
     SVO_HIP(hipSetDevice(p->ctx->device));
     SVO_HIP(set_join(p));
     const uint8_t* src = p->d_base + (size_t)frame * p->stride + (gradient ? p->grad_off : 0) + p->geom.off[level];
-    SVO_HIP(hipMemcpyAsync(out, src, (size_t)p->geom.w[level] * p->geom.h[level], hipMemcpyDeviceToHost, p->ctx->stream));
-    SVO_HIP(hipStreamSynchronize(p->ctx->stream));
+    SVO_HIP(hipMemcpyAsync(out, src, (size_t)p->geom.w[level] * p->geom.h[level], hipMemcpyDeviceToHost, ctx_stream(p->ctx)));
+    SVO_HIP(hipStreamSynchronize(ctx_stream(p->ctx)));
     return SVO_OK;
 }
 
@@ -561,7 +585,7 @@ int svo_align_batch_create(svo_ctx* c, const svo_camera* cam, const svo_align_pa
 int svo_align_batch_destroy(svo_align_batch* b) {
     if (!b) return SVO_OK;
     (void)hipSetDevice(b->ctx->device);
-    (void)hipStreamSynchronize(b->ctx->stream);
+    (void)hipStreamSynchronize(ctx_stream(b->ctx));
     free_batch(b);
     delete b;
     return SVO_OK;
@@ -608,7 +632,7 @@ int svo_align_batch_set_pair(svo_align_batch* b, int32_t pair, const svo_pyramid
     d.n_kf = n_kf;
     const size_t fo = (size_t)pair * b->max_f;
     svo_ctx* c = b->ctx;
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
     // stage the pair's arrays in the context's pinned ring and return without waiting: the copies are
     // ordered before any later work on the stream, and the ring drains when it wraps or another call
     // needs the pinned block (large pairs, or no pinned memory: direct copies and a wait, as before)
@@ -718,7 +742,7 @@ int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, 
         if (b->d_stage) {  // a scatter queued on the stream, or an upload left on the copy stream by an
                            // earlier call's error exit, may still touch the old block
             SVO_HIP(hipStreamSynchronize(b->ctx->copy));
-            SVO_HIP(hipStreamSynchronize(b->ctx->stream));
+            SVO_HIP(hipStreamSynchronize(ctx_stream(b->ctx)));
             SVO_HIP(hipFree(b->d_stage));
         }
         b->d_stage = nullptr;
@@ -727,7 +751,7 @@ int svo_align_batch_set_pairs(svo_align_batch* b, int32_t first, int32_t count, 
         b->stage_bytes = need + need / 4;
     }
     svo_ctx* c = b->ctx;
-    hipStream_t s = c->stream, cs = c->copy;
+    hipStream_t s = ctx_stream(c), cs = c->copy;
     SVO_HIP(ctx_ring_drain(c));  // set_pair copies still reading the ring go first (stream order anyway)
     // the upload runs on the copy stream, behind only the previous scatter out of staging (not behind
     // whatever else `stream` holds, e.g. the pyramid build these pairs read); `stream` then waits for it
@@ -774,8 +798,8 @@ int svo_align_batch_set_initial_poses(svo_align_batch* b, const double* poses) {
     SVO_HIP(hipSetDevice(b->ctx->device));
     for (int32_t i = 0; i < b->n_pairs; ++i) std::memcpy(b->h_pairs[i].cur_pose, poses + 7 * i, 7 * sizeof(double));
     SVO_HIP(hipMemcpyAsync(b->d_pairs, b->h_pairs.data(), sizeof(svo::PairDesc) * b->n_pairs, hipMemcpyHostToDevice,
-                           b->ctx->stream));
-    SVO_HIP(hipStreamSynchronize(b->ctx->stream));
+                           ctx_stream(b->ctx)));
+    SVO_HIP(hipStreamSynchronize(ctx_stream(b->ctx)));
     return SVO_OK;
 }
 
@@ -833,7 +857,7 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
     // SVO_CHAINS=1 (measurement knob, read once): the whole batch as one chain
     static const bool one_chain = getenv("SVO_CHAINS") && atoi(getenv("SVO_CHAINS")) == 1;
     if (marks || b->n_pairs < kSplitMin || one_chain) {
-        svo::launch_align(a, c->stream, marks);
+        svo::launch_align(a, ctx_stream(c), marks);
     } else {
         // two independent half-batch chains on two streams: one chain's latency-bound stages (the
         // per-pair robust scale) overlap the other chain's feature stages.  Results are per pair and
@@ -856,18 +880,30 @@ static int run_batch(svo_align_batch* b, hipEvent_t* marks) {
                                              : (b->params.median_mode == SVO_MEDIAN_REFERENCE && !k2v ? 2 : 0);
         if (stagger < 0 || stagger > 1 + 3 * (b->params.max_level - b->params.min_level + 1))
             return fail(SVO_ERR_ARG, "SVO_STAGGER=%d outside the chain's launch marks", stagger);
-        SVO_HIP(hipEventRecord(c->fork, c->stream));
-        for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->fork, 0));
+        // Chains join the context stream lazily (svo_ctx::pending_batch): a run that follows a run of this same batch
+        // and split, with nothing else queued in between, lets chain i follow its own previous run on its own stream
+        // (chain i reads and writes only its own pairs) instead of forking after every chain of that run.
+        static const bool defer = !getenv("SVO_DEFER_JOIN") || atoi(getenv("SVO_DEFER_JOIN")) != 0;  // (read once)
+        const bool lazy = defer && stagger == 0;
+        const bool cont = lazy && c->pending_batch == b && c->pending_chains == ns;
+        hipStream_t s0 = cont ? c->stream_raw : ctx_stream(c);  // (ctx_stream joins any other pending chains)
+        if (!cont) {
+            SVO_HIP(hipEventRecord(c->fork, s0));
+            for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->fork, 0));
+        }
         for (int i = 0; i < ns; ++i) {
             const int32_t p0 = i * per, cnt = i == ns - 1 ? b->n_pairs - p0 : std::min(per, b->n_pairs - p0);
             if (cnt <= 0) break;  // (later chains would be empty too)
             if (i >= 1 && stagger > 0) SVO_HIP(hipStreamWaitEvent(c->sides[i], c->chain_marks[i - 1][stagger], 0));
-            svo::launch_align(sub_batch(a, b, p0, cnt), i == 0 ? c->stream : c->sides[i],
+            svo::launch_align(sub_batch(a, b, p0, cnt), i == 0 ? s0 : c->sides[i],
                               i < ns - 1 && stagger > 0 ? c->chain_marks[i] : nullptr);
         }
-        for (int i = 1; i < ns; ++i) {
-            SVO_HIP(hipEventRecord(c->joins[i], c->sides[i]));
-            SVO_HIP(hipStreamWaitEvent(c->stream, c->joins[i], 0));
+        for (int i = 1; i < ns; ++i) SVO_HIP(hipEventRecord(c->joins[i], c->sides[i]));
+        if (lazy) {
+            c->pending_batch = b;  // joined by the next ctx_stream()
+            c->pending_chains = ns;
+        } else {
+            for (int i = 1; i < ns; ++i) SVO_HIP(hipStreamWaitEvent(s0, c->joins[i], 0));
         }
     }
     SVO_HIP(hipGetLastError());
@@ -906,7 +942,7 @@ int svo_align_batch_results(svo_align_batch* b, double* poses, double* err, int3
     if (!b->ran) return fail(SVO_ERR_STATE, "batch has not been run");
     SVO_HIP(hipSetDevice(b->ctx->device));
     svo_ctx* c = b->ctx;
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
     const size_t np = (size_t)b->n_pairs, bp = np * 7 * sizeof(double), be = np * sizeof(double), bs = np * sizeof(int32_t);
     void* host = nullptr;
     if (ctx_pinned(c, bp + be + bs, &host) == hipSuccess) {  // through the pinned block: kernel copies (stage_copy)
@@ -938,14 +974,14 @@ int svo_align_batch_traces(svo_align_batch* b, int32_t pair, svo_level_trace* ou
     svo_ctx* c = b->ctx;
     void* host = nullptr;
     if (ctx_pinned(c, bytes, &host) == hipSuccess) {  // a kernel copy through the pinned block (as results)
-        SVO_HIP(stage_copy(c, host, b->d_traces + (size_t)pair * L, bytes, hipMemcpyDeviceToHost, c->stream));
-        SVO_HIP(hipStreamSynchronize(c->stream));
+        SVO_HIP(stage_copy(c, host, b->d_traces + (size_t)pair * L, bytes, hipMemcpyDeviceToHost, ctx_stream(c)));
+        SVO_HIP(hipStreamSynchronize(ctx_stream(c)));
         std::memcpy(out, host, bytes);
         return SVO_OK;
     }
     (void)hipGetLastError();
-    SVO_HIP(hipMemcpyAsync(out, b->d_traces + (size_t)pair * L, bytes, hipMemcpyDeviceToHost, c->stream));
-    SVO_HIP(hipStreamSynchronize(c->stream));
+    SVO_HIP(hipMemcpyAsync(out, b->d_traces + (size_t)pair * L, bytes, hipMemcpyDeviceToHost, ctx_stream(c)));
+    SVO_HIP(hipStreamSynchronize(ctx_stream(c)));
     return SVO_OK;
 }
 
@@ -984,14 +1020,14 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
     double* d_v = static_cast<double*>(base);
     uint32_t* d_sel = reinterpret_cast<uint32_t*>(d_v + q);
     double* d_out = reinterpret_cast<double*>(d_sel + sel_stride);
-    SVO_HIP(hipMemsetAsync(d_out, 0, (size_t)(kDiag + ntr) * 8, c->stream));
-    SVO_HIP(hipMemcpyAsync(d_v, values, (size_t)n_slots * 8, hipMemcpyHostToDevice, c->stream));
+    SVO_HIP(hipMemsetAsync(d_out, 0, (size_t)(kDiag + ntr) * 8, ctx_stream(c)));
+    SVO_HIP(hipMemcpyAsync(d_v, values, (size_t)n_slots * 8, hipMemcpyHostToDevice, ctx_stream(c)));
     if (svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, sel_stride, impl, d_out,
-                                       ntr ? d_out + kDiag : nullptr, (uint32_t)ntr, c->stream) != 0)
+                                       ntr ? d_out + kDiag : nullptr, (uint32_t)ntr, ctx_stream(c)) != 0)
         return fail(SVO_ERR_ARG, "the vector does not fit the requested kernel");
     SVO_HIP(hipGetLastError());
-    SVO_HIP(hipMemcpyAsync(out, d_out, (size_t)std::min<int64_t>(out_len, kDiag + ntr) * 8, hipMemcpyDeviceToHost, c->stream));
-    SVO_HIP(hipStreamSynchronize(c->stream));
+    SVO_HIP(hipMemcpyAsync(out, d_out, (size_t)std::min<int64_t>(out_len, kDiag + ntr) * 8, hipMemcpyDeviceToHost, ctx_stream(c)));
+    SVO_HIP(hipStreamSynchronize(ctx_stream(c)));
     return SVO_OK;
 }
 
@@ -1001,7 +1037,7 @@ static int feature_align_impl(svo_ctx* c, const svo_camera* cam, int32_t patch_s
                               const svo_pyramid_set* cur_set, int32_t cur_frame, int32_t n, const double* ref_px,
                               double* px_inout, double* err, int32_t* status) {
     SVO_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
     // one block, same layout on both sides: ref planes | ref px | px | err | status (8-B aligned pieces);
     // one H2D copy of the inputs (planes .. px) and one D2H copy of the outputs (px .. status)
     const size_t nn = (size_t)n;
@@ -1228,7 +1264,7 @@ int svo_depth_update(svo_ctx* c, const svo_camera* cam, int32_t n_kf, const svo_
     *n_cand = 0;
     if (n == 0) return SVO_OK;
     SVO_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
     svo::DepthArgs a{};
     // one block, same layout on both sides: inputs (seeds | keyframe poses | keyframe planes | cur pose),
     // outputs (counts | survivors | outcomes | candidate points | candidate seeds), device-only scratch
@@ -1315,7 +1351,7 @@ static int fs_check(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t
 static int fs_detect(svo_ctx* c, const svo_pyramid_set* p, int32_t frame, int32_t threshold, int32_t capacity,
                      uint32_t* keys, int32_t* n) {
     SVO_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
     const int64_t npx = (int64_t)p->width * p->height;
     const int nseg = svo::feature_detect_segments(npx);
     void* base = nullptr;
@@ -1408,7 +1444,7 @@ int svo_feature_select_by_value(svo_ctx* c, const svo_pyramid_set* p, int32_t fr
     if (cell_size < 1 || cell_size > 1024) return fail(SVO_ERR_ARG, "cell_size must be in [1, 1024]");
     const int32_t W = p->width, H = p->height, gr = H / cell_size + 1, gc = W / cell_size + 1, nc = gr * gc;
     SVO_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
     void* base = nullptr;
     hipError_t e = ctx_scratch(c, (size_t)nc * 5 + 64, &base);
     if (e != hipSuccess) return fail(SVO_ERR_HIP, "svo_feature_select_by_value: %s", hipGetErrorString(e));
@@ -1502,7 +1538,7 @@ int svo_pose_optimize(svo_ctx* c, int32_t n_frames, const int32_t* feat_off, con
             return fail(SVO_ERR_ARG, "feature %lld: visible from the previous call but without a point "
                                      "(the reference dereferences a null m_point)", (long long)k);
     SVO_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
+    hipStream_t s = ctx_stream(c);
     // one block, same layout on both sides: inputs (offsets | poses | bearing | point | has_point | flags)
     // then outputs (poses | err | status | flags) then device-only scratch (rows | weights); one H2D copy
     // of the inputs and one D2H copy of the outputs through the context's pinned staging

@@ -154,6 +154,36 @@ def main():
             inflation.append((t1s.max() - t0s.min()) * TICK_US / np.median(dur))
     k1 = r[r["kind"] == 1]
     k3 = r[r["kind"] == 3]
+
+    def wg_stats(rows):  # per-workgroup durations by level (workgroups that returned at once excluded: < 2 us)
+        d = (rows["t1"] - rows["t0"]).astype(np.float64) * TICK_US
+        keep = d >= 2.0
+        out = {}
+        for l in np.unique(rows["level"]):
+            m = keep & (rows["level"] == l)
+            if m.any():
+                out[int(l)] = {"workgroups": int(m.sum()), "median_us": round(float(np.median(d[m])), 1),
+                               "p90_us": round(pct(d[m], 90), 1)}
+        return out
+
+    # co-residency: for each K1 / K3 workgroup, the mean number of K1 / K3 workgroups resident on its CU over its life
+    def coresidency(kinds):
+        vals = []
+        for c_, kd in per_cu.items():
+            iv = sorted(x for k in kinds for x in kd.get(k, []))
+            if not iv:
+                continue
+            ev = sorted([(s_, 1) for s_, _ in iv] + [(e_, -1) for _, e_ in iv])
+            cur, last, area, busy = 0, ev[0][0], 0, 0
+            for t, dlt in ev:
+                if cur > 0:
+                    area += cur * (t - last)
+                    busy += t - last
+                cur += dlt
+                last = t
+            if busy:
+                vals.append(area / busy)
+        return round(float(np.mean(vals)), 2) if vals else None
     out = {
         "workload": f"config 2 headline: {P} pairs ({D} distinct scenes), {NF} features, patch {PATCH}, {L} levels, "
                     f"reference median semantics, cell order; diagnostic build (make timeline)",
@@ -172,11 +202,39 @@ def main():
                           "slowest_pair_median": round(float(np.median(slowest)), 1),
                           "span_over_median_pair": round(float(np.median(inflation)), 3)},
         "k1_workgroups": int(len(k1)), "k3_workgroups": int(len(k3)),
+        "k1_workgroup_us_by_level": wg_stats(k1), "k3_workgroup_us_by_level": wg_stats(k3),
+        "k1k3_workgroups_resident_per_busy_cu": coresidency((1, 3)),
         "lower_bounds_ms": {
             "k2v_only": round(float(d2.sum()) / 256 / args.steps / 1e3, 4),
             "k2v_plus_k1k3_cu_time": round((float(d2.sum()) + cu_time["K1|K3"]) / 256 / args.steps / 1e3, 4)},
     }
-    print(json.dumps(out, indent=1))
+    # CU occupancy over time, in 25 us bins from the first workgroup start: CUs holding a K2V workgroup, CUs holding
+    # only K1 / K3 workgroups, idle CUs (every step; the step boundaries show as the idle peaks)
+    binw = 2500  # ticks (25 us)
+    nb = int((int(r["t1"].max()) - t_first) // binw) + 1
+    k2b = np.zeros(nb)
+    k13b = np.zeros(nb)
+    for c_, kd in per_cu.items():
+        for kinds, acc in (((2,), k2b), ((1, 3), k13b)):
+            iv = sorted(x for k in kinds for x in kd.get(k, []))
+            merged = []
+            for s_, e_ in iv:
+                if merged and s_ <= merged[-1][1]:
+                    merged[-1][1] = max(merged[-1][1], e_)
+                else:
+                    merged.append([s_, e_])
+            for s_, e_ in merged:
+                a0, a1 = s_ - t_first, e_ - t_first
+                for b_ in range(int(a0 // binw), int(a1 // binw) + 1):
+                    lo_, hi_ = max(a0, b_ * binw), min(a1, (b_ + 1) * binw)
+                    if hi_ > lo_:
+                        acc[b_] += (hi_ - lo_) / binw
+    k13b = np.minimum(k13b, 256 - k2b)
+    out["occupancy_25us_bins"] = {"k2v_cus": [round(x, 1) for x in k2b], "k1k3_only_cus": [round(x, 1) for x in k13b],
+                                  "idle_cus": [round(256 - a - b_, 1) for a, b_ in zip(k2b, k13b)]}
+    print(json.dumps({k: v for k, v in out.items() if k != "occupancy_25us_bins"}, indent=1))
+    idle = out["occupancy_25us_bins"]["idle_cus"]
+    print("idle CUs per 25 us bin:", " ".join(f"{x:.0f}" for x in idle))
     if args.json:
         with open(args.json, "w") as f:
             json.dump(out, f, indent=1)
