@@ -71,6 +71,8 @@ def parse():
                          "per-launch bytes assume every align dispatch belongs to the P-pair chain")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="no GPU: each rank's step is the CPU oracle on its pairs (exercises the multi-rank path)")
+    ap.add_argument("--kernel-stats", default=os.path.join(ROOT, "profiles", "headline_kernel_stats.csv"),
+                    help="tools/headline_kernel_stats.py output of a headline-only kernel trace (roofline.dominant_kernel)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC traffic summary of this workload (tools/pmc_traffic.py output)")
     return ap.parse_args()
@@ -390,6 +392,7 @@ def main():
         if pm.get("pairs") == P and pm.get("features") == nf and pm.get("levels") == L and pm.get("patch") == patch:
             traffic = pm.get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(args.pmc_json, ROOT)
+    dominant = dominant_kernel(args.kernel_stats, P, n_chains(P, mode), b_pair, L) if mode == svo_amd.MEDIAN_REFERENCE else None
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
@@ -408,7 +411,8 @@ def main():
                      "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes_per_launch": b_pair * P,
                      "algorithmic_bytes_per_pair": b_pair, "traffic_source": traffic_src,
                      "stages_ms": {k: round(v, 4) for k, v in stages.items()},
-                     "dominant_stage": max(stages, key=stages.get)},
+                     "dominant_stage": max(stages, key=stages.get),
+                     "dominant_kernel": dominant},
         # the co-limiting roof SURVEY 8(d) names: ~1900 algorithmic fp64 flop per feature and level
         # (bilinear blends, Jacobian, SE3 / projection, weights, 5 factored accumulators, 21 x 3 expansion)
         "roofline_fp64_valu": {"achieved": round(1900.0 * nf * L * P / (kernel_ms * 1e-3) / 1e12, 3),
@@ -467,6 +471,32 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def dominant_kernel(path, P, chains, b_pair, L):
+    """The dominant kernel's roofline from a committed headline-only kernel trace (profiles/headline_kernel_stats.csv,
+    tools/headline_kernel_stats.py): K2V's median duration per launch of P / chains pairs, its algorithmic bytes per
+    launch (one level of b_pair per pair: the level's share of the three stacks and the features), the HBM fraction.
+    Tracked-file arithmetic only (the live figure is the chain's, above); None without a matching file."""
+    if not path or not os.path.exists(path):
+        return None
+    import csv
+    per = P // chains
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["kernel"].startswith("void align_scale_refv_kernel") and int(r["grid_x"]) == per * int(r["workgroup_x"]):
+                us = float(r["median_us"])
+                byt = per * b_pair / L
+                return {"name": "align_scale_refv_kernel (K2V)", "pairs_per_launch": per, "launch_median_us": us,
+                        "launches_in_trace": int(r["count"]), "algorithmic_bytes_per_launch": round(byt),
+                        "achieved_GBps": round(byt / (us * 1e-6) / 1e9, 1),
+                        "frac": round(byt / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
+                        # a launch holds one CU per pair: 256 / per launches fill the chip side by side
+                        "frac_chip": round(byt / (us * 1e-6) / 1e9 / HBM_PEAK_GBS * 256 / per, 5),
+                        "note": "one launch = one level of a chain's pairs on one CU each; frac_chip counts the "
+                                "256 / pairs_per_launch launches that run side by side; latency-bound (DESIGN 16, 19)",
+                        "source": os.path.relpath(path, ROOT)}
+    return None
 
 
 def n_chains(P, mode):
