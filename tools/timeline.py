@@ -208,6 +208,22 @@ def main():
             "k2v_only": round(float(d2.sum()) / 256 / args.steps / 1e3, 4),
             "k2v_plus_k1k3_cu_time": round((float(d2.sum()) + cu_time["K1|K3"]) / 256 / args.steps / 1e3, 4)},
     }
+    # per pair and level, its K2V durations over the steps (does a pair's cost at one level predict the next?)
+    per_pair = defaultdict(list)
+    for row, d in zip(k2, d2):
+        per_pair[(int(row["pair_base"]) + int(row["block"]), int(row["level"]))].append(float(d))
+    pairs_idx = sorted({p_ for p_, _ in per_pair})
+    lv = sorted({l_ for _, l_ in per_pair}, reverse=True)
+    mat = np.array([[np.mean(per_pair.get((p_, l_), [np.nan])) for l_ in lv] for p_ in pairs_idx])
+    corr = {}
+    for i in range(len(lv) - 1):
+        a_, b_ = mat[:, i], mat[:, i + 1]
+        ok = ~np.isnan(a_) & ~np.isnan(b_)
+        corr[f"L{lv[i]}->L{lv[i + 1]}"] = round(float(np.corrcoef(a_[ok], b_[ok])[0, 1]), 3) if ok.sum() > 2 else None
+    out["k2v_pair_duration_corr_between_levels"] = corr
+    # the same pair and level in different steps (run-to-run repeatability of a pair's K2V time)
+    rep = [np.std(v) / np.mean(v) for v in per_pair.values() if len(v) > 1]
+    out["k2v_pair_duration_cv_across_steps_median"] = round(float(np.median(rep)), 4) if rep else None
     # CU occupancy over time, in 25 us bins from the first workgroup start: CUs holding a K2V workgroup, CUs holding
     # only K1 / K3 workgroups, idle CUs (every step; the step boundaries show as the idle peaks)
     binw = 2500  # ticks (25 us)
