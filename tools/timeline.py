@@ -224,6 +224,31 @@ def main():
     # the same pair and level in different steps (run-to-run repeatability of a pair's K2V time)
     rep = [np.std(v) / np.mean(v) for v in per_pair.values() if len(v) > 1]
     out["k2v_pair_duration_cv_across_steps_median"] = round(float(np.median(rep)), 4) if rep else None
+    # one chain's critical path: per (chain, step) the launches in order K1 K2V K3 per level; each launch's span (first
+    # workgroup start to last end) and the gap from the previous launch's last end to its first start
+    launches_all = defaultdict(list)
+    for row in r:
+        launches_all[(int(row["pair_base"]), int(row["level"]), int(row["kind"]))].append((int(row["t0"]), int(row["t1"])))
+    spans_k = defaultdict(list)
+    gaps_k = defaultdict(list)
+    order = [(l_, k_) for l_ in sorted({int(x) for x in r["level"]}, reverse=True) for k_ in (1, 2, 3)]
+    for pb in sorted({int(x) for x in r["pair_base"]}):
+        seq = []
+        for l_, k_ in order:
+            iv = sorted(launches_all.get((pb, l_, k_), []))
+            n_per = len(iv) // args.steps if iv else 0
+            for st_ in range(args.steps):
+                grp = sorted(iv, key=lambda x: x[0])[st_ * n_per:(st_ + 1) * n_per] if n_per else []
+                if grp:
+                    seq.append((st_, l_, k_, min(x[0] for x in grp), max(x[1] for x in grp)))
+        seq.sort(key=lambda x: x[3])
+        for i_, (st_, l_, k_, a0, a1) in enumerate(seq):
+            spans_k[KIND[k_]].append((a1 - a0) * TICK_US)
+            if i_:
+                gaps_k[KIND[k_]].append((a0 - seq[i_ - 1][4]) * TICK_US)
+    out["chain_launch_span_us_median"] = {k: round(float(np.median(v)), 1) for k, v in spans_k.items()}
+    out["chain_gap_before_launch_us_median"] = {k: round(float(np.median(v)), 1) for k, v in gaps_k.items()}
+    out["chain_gap_before_launch_us_mean"] = {k: round(float(np.mean(v)), 1) for k, v in gaps_k.items()}
     # CU occupancy over time, in 25 us bins from the first workgroup start: CUs holding a K2V workgroup, CUs holding
     # only K1 / K3 workgroups, idle CUs (every step; the step boundaries show as the idle peaks)
     binw = 2500  # ticks (25 us)
