@@ -1165,8 +1165,11 @@ struct VSel {
     // (vec[nth - 1], vec[nth]) of the post-state, on thread 0
     // preload_next: load the raw rows for the MAD pass while wave 0 runs this pass's one-wave rounds (the other
     // waves' registers are free after the dump); returns through `preloaded` whether it did
+    // retire (the last pass): once the segment has gone to wave 0's one-wave rounds, waves 1-7 end here instead of
+    // waiting at the pass's remaining barriers; an ended wave frees its SIMD's registers for other kernels' workgroups
+    // and no longer counts at s_barrier.  `retired` tells the caller to return.
     __device__ __forceinline__ void select(const double* src, bool mad, double med, bool preloaded, bool preload_next,
-                                           double& hi, double& lo, bool& did_preload) {
+                                           double& hi, double& lo, bool& did_preload, bool retire, bool& retired) {
         const uint64_t t0 = dg ? clock64() : 0;
         uint64_t tstamp = t0;
         did_preload = false;
@@ -1212,6 +1215,12 @@ struct VSel {
             const uint32_t f0 = f;
             dump(seg, f0, sh.mbx + kMbCap);
             __syncthreads();
+#if !defined(SVO_K2V_KEEP_WAVES)
+            if (retire && !preload_next && wave != 0) {  // (not in the debug kernel: kRetire false)
+                retired = true;
+                return;
+            }
+#endif
             did_preload = preload_next;
             if (preload_next && wave != 0) {
                 load_raw(src);
@@ -1262,7 +1271,7 @@ struct VSel {
 
 // computeMedian / computeMAD (src/algorithm.cpp:834-865) with the reference's post-state; every thread
 // returns med and mad.  M slots, n visible.
-template <class L>
+template <class L, bool kRetire>  // kRetire: waves 1-7 end after the last pass's dump (the product kernel only)
 __device__ __forceinline__ void refv_robust_scale(const double* src, VShared<L>& sh, double* gseg, VDiag* dg, uint32_t M,
                                                   uint32_t n, double& med, double& mad) {
     L::Rows::fence();
@@ -1278,8 +1287,9 @@ __device__ __forceinline__ void refv_robust_scale(const double* src, VShared<L>&
     for (int P = 0; P < 2; ++P) {  // one copy of the selection for both passes
         s.P = P;
         double lo = 0.0, hi = 0.0;
-        bool did = false;
-        s.select(src, P == 1, m0, pre, P == 0 && L::kPreload, hi, lo, did);
+        bool did = false, retired = false;
+        s.select(src, P == 1, m0, pre, P == 0 && L::kPreload, hi, lo, did, kRetire && P == 1, retired);
+        if (retired) return;  // (waves 1-7 after the last pass's dump: only thread 0's med / mad are used)
         pre = did;
         if (s.tid == 0) sh.bcd = even ? (lo + hi) / 2.0 : hi;
         __syncthreads();
@@ -1315,7 +1325,7 @@ __device__ __forceinline__ void scale_refv_pair(const AlignArgs& a, VShared<L>& 
     const uint32_t n = ncv * (uint32_t)a.area;
     double med = kDblMax, mad = 0.0;  // n == 0: every slot is DBL_MAX in the reference
     if (n > 0)
-        refv_robust_scale<L>(a.scratch + (int64_t)pair * a.key_stride, sh,
+        refv_robust_scale<L, true>(a.scratch + (int64_t)pair * a.key_stride, sh,
                              reinterpret_cast<double*>(a.sel + (int64_t)pair * a.sel_stride), nullptr, M, n, med, mad);
     if (tid == 0) {
         double sigma = 1.482602218505602 * mad;
@@ -1359,7 +1369,7 @@ __global__ void __launch_bounds__(kVT, 1) debug_robust_scale_v_kernel(const doub
     }
     __syncthreads();
     double med = 0.0, mad = 0.0;
-    refv_robust_scale<L>(v, sh, gseg, &dg, M, n, med, mad);
+    refv_robust_scale<L, false>(v, sh, gseg, &dg, M, n, med, mad);
     if (threadIdx.x == 0) {
         out[0] = med;
         out[1] = mad;
