@@ -176,7 +176,10 @@ int svo_align_batch_set_pairs(svo_align_batch* batch, int32_t first, int32_t cou
 /* Replace the initial cur poses of all pairs (n_pairs x 7).  Synchronous H2D. */
 int svo_align_batch_set_initial_poses(svo_align_batch* batch, const double* poses);
 /* Run every pair.  Asynchronous on the context stream; inputs stay untouched, so repeated runs are
- * identical (the result pose is written to a separate device buffer). */
+ * identical (the result pose is written to a separate device buffer).  A large reference-mode batch runs as
+ * sub-batch chains on the context's side streams; back-to-back runs of the same batch are ordered per chain (each
+ * chain touches only its own pairs), and every other call that uses the context (results, traces, set_pair(s),
+ * pyramid uploads / builds, FeatureAlignment, events, synchronize, destroy) first waits for all of them. */
 int svo_align_batch_run(svo_align_batch* batch);
 /* One run with a hipEvent between consecutive kernel launches (diagnostics; synchronous).  stage_ms[5]
  * receives the device time per stage summed over the levels: [0] world points + state, [1] residuals,
