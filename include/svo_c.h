@@ -209,6 +209,8 @@ enum { SVO_SCALE_AUTO = 0, SVO_SCALE_K2R = 1, SVO_SCALE_K2V = 2, SVO_SCALE_K2 = 
  *        (tools/k2r_probe.py).
  * K2V with out_len > 206: out[206..] receives a round trace (development): per round 8 header doubles (pass + 10
  * kind, f, l, pivot, Ks, #GE, #LE, cut) and the vector's n_slots values after the round.
+ * K2V with out_len == 2: no diagnostics; the vector runs through the product kernel's own code path (its layouts
+ * and one-wave size), whereas the diagnostics kernel hands segments of <= 1024 positions to wave 0.
  * Synchronous.  SVO_ERR_ARG if impl is K2V and the vector does not fit it. */
 int svo_debug_robust_scale(svo_ctx* ctx, const double* values, int64_t n_slots, int64_t n_valid, int32_t impl,
                            double* out, int64_t out_len);

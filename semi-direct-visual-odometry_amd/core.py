@@ -1090,7 +1090,8 @@ def debug_robust_scale(values, n_valid, ctx=None, impl=SCALE_AUTO, diagnostics=F
     include/svo_c.h).  values: the full residual vector, invisible slots = DBL_MAX (src/optimizer.cpp:387-396)."""
     ctx = ctx or default_context()
     v = np.ascontiguousarray(values, np.float64)
-    out = np.zeros(206)
+    # without diagnostics only med / mad come back, and K2V runs the product kernel's own code path (svo_c.h)
+    out = np.zeros(206 if diagnostics else 2)
     check(lib().svo_debug_robust_scale(ctx.handle, ptr(v), len(v), int(n_valid), int(impl), ptr(out), len(out)))
     if diagnostics:
         return float(out[0]), float(out[1]), out[2:].copy()

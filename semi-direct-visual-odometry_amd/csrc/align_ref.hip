@@ -822,11 +822,11 @@ void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s) {
     else hipLaunchKernelGGL((align_scale_ref_kernel<17, 8>), dim3(a.n_pairs), dim3(Geo<8>::RT), 0, s, a, level);
 }
 int launch_debug_robust_scale(const double* v, uint32_t M, uint32_t n, uint32_t* sel, int64_t sel_stride, int impl,
-                              double* out, double* trace, uint32_t trcap, hipStream_t s) {
+                              double* out, double* trace, uint32_t trcap, hipStream_t s, bool plain) {
     if (impl == SVO_SCALE_AUTO) impl = M <= (uint32_t)refv_max_slots() ? SVO_SCALE_K2V : SVO_SCALE_K2R;
     if (impl == SVO_SCALE_K2V) {
         if (M > (uint32_t)refv_max_slots()) return -1;
-        launch_debug_robust_scale_v(v, M, n, reinterpret_cast<double*>(sel), out, trace, trcap, s);
+        launch_debug_robust_scale_v(v, M, n, reinterpret_cast<double*>(sel), out, trace, trcap, s, plain);
         return 0;
     }
     // (SVO_K2R_WAVES=16: the 16-wave instantiation, as small batches run it)

@@ -55,7 +55,7 @@ constexpr int kVW = kVT / 64;         // waves
 // mailbox holds no more) continue on wave 0 (its rows 0 .. OW / 64 - 1); wave 0's register rows for the MAD pass are staged by the other waves during its one-wave rounds
 // past the one-wave segment and its mailbox (mbx[2 OW, ...))
 #ifndef SVO_ONEWAVE
-#define SVO_ONEWAVE 1024
+#define SVO_ONEWAVE 2048
 #endif
 constexpr int kRowPad = 128;          // record planes: rows padded to two groups of 64 lanes
 
@@ -87,6 +87,11 @@ using LayB = Lay<RowsB, 118, 4352, false, SVO_ONEWAVE>;  // 60 416 slots: 92 reg
 // mailbox (163 032 of the CU's 163 840 LDS bytes in all), so the large rounds exchange in chunks, each walking only its
 // own steps (LayC's kernels keep their compiler code below v64)
 using LayC = Lay<RowsC, 128, 1344, false, 512>;
+// the debug kernel (svo_debug_robust_scale: round traces, diagnostics) runs LayA / LayB with 1024-position one-wave
+// rounds: its diagnostics need registers that the 2048-position one-wave code leaves below neither fence (v80 / v72).
+// Both sizes run the same introselect rounds; only the point where wave 0 takes the segment over differs
+using LayADbg = Lay<RowsA, 98, 12288, true, 1024>;
+using LayBDbg = Lay<RowsB, 118, 4352, false, 1024>;
 
 template <class L>
 struct VShared {
@@ -1389,6 +1394,20 @@ __global__ void __launch_bounds__(kVT, 1) debug_robust_scale_v_kernel(const doub
     }
 }
 
+// svo_debug_robust_scale with out_len 2: the product kernel's code path (its layouts, 2048-position one-wave rounds,
+// waves 1-7 retiring) on an arbitrary vector; out[0..1] med / mad
+template <class L>
+__global__ void __launch_bounds__(kVT, 1) plain_robust_scale_v_kernel(const double* v, uint32_t M, uint32_t n, double* gseg,
+                                                                      double* out) {
+    __shared__ VShared<L> sh;
+    double med = 0.0, mad = 0.0;
+    refv_robust_scale<L, true>(v, sh, gseg, nullptr, M, n, med, mad);
+    if (threadIdx.x == 0) {
+        out[0] = med;
+        out[1] = mad;
+    }
+}
+
 int64_t refv_max_slots() { return LayC::kCap; }
 // the smaller layout (more mailbox, the MAD rows preloaded) whenever every pair of the launch fits it
 void launch_scale_refv(const AlignArgs& a, int level, hipStream_t s) {
@@ -1400,11 +1419,20 @@ void launch_scale_refv(const AlignArgs& a, int level, hipStream_t s) {
         hipLaunchKernelGGL(align_scale_refv_kernel<LayC>, dim3(a.n_pairs), dim3(kVT), 0, s, a, level);
 }
 void launch_debug_robust_scale_v(const double* v, uint32_t M, uint32_t n, double* gseg, double* out, double* trace,
-                                 uint32_t trcap, hipStream_t s) {
-    if (M <= LayA::kCap)
-        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayA>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
-    else if (M <= LayB::kCap)
-        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayB>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
+                                 uint32_t trcap, hipStream_t s, bool plain) {
+    if (plain) {
+        if (M <= LayA::kCap)
+            hipLaunchKernelGGL(plain_robust_scale_v_kernel<LayA>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out);
+        else if (M <= LayB::kCap)
+            hipLaunchKernelGGL(plain_robust_scale_v_kernel<LayB>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out);
+        else
+            hipLaunchKernelGGL(plain_robust_scale_v_kernel<LayC>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out);
+        return;
+    }
+    if (M <= LayADbg::kCap)
+        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayADbg>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
+    else if (M <= LayBDbg::kCap)
+        hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayBDbg>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
     else
         hipLaunchKernelGGL(debug_robust_scale_v_kernel<LayC>, dim3(1), dim3(kVT), 0, s, v, M, n, gseg, out, trace, trcap);
 }

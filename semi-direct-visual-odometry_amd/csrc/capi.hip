@@ -1022,8 +1022,9 @@ int svo_debug_robust_scale(svo_ctx* c, const double* values, int64_t n_slots, in
     double* d_out = reinterpret_cast<double*>(d_sel + sel_stride);
     SVO_HIP(hipMemsetAsync(d_out, 0, (size_t)(kDiag + ntr) * 8, ctx_stream(c)));
     SVO_HIP(hipMemcpyAsync(d_v, values, (size_t)n_slots * 8, hipMemcpyHostToDevice, ctx_stream(c)));
+    // out_len 2 (med / mad only): K2V runs the product kernel's own code path instead of the debug kernel
     if (svo::launch_debug_robust_scale(d_v, (uint32_t)n_slots, (uint32_t)n_valid, d_sel, sel_stride, impl, d_out,
-                                       ntr ? d_out + kDiag : nullptr, (uint32_t)ntr, ctx_stream(c)) != 0)
+                                       ntr ? d_out + kDiag : nullptr, (uint32_t)ntr, ctx_stream(c), out_len == 2) != 0)
         return fail(SVO_ERR_ARG, "the vector does not fit the requested kernel");
     SVO_HIP(hipGetLastError());
     SVO_HIP(hipMemcpyAsync(out, d_out, (size_t)std::min<int64_t>(out_len, kDiag + ntr) * 8, hipMemcpyDeviceToHost, ctx_stream(c)));

@@ -80,15 +80,16 @@ struct AlignArgs {
 void launch_align(const AlignArgs& a, hipStream_t s, hipEvent_t* marks = nullptr);  // marks: see align.hip
 void launch_scale_ref(const AlignArgs& a, int level, hipStream_t s);                 // K2R (align_ref.hip)
 // svo_debug_robust_scale: impl SVO_SCALE_*; returns -1 if the vector does not fit the requested kernel
+// plain (K2V): the product kernel's own code path (no diagnostics, out[0..1] only) instead of the debug kernel
 int launch_debug_robust_scale(const double* v, uint32_t M, uint32_t n, uint32_t* sel, int64_t sel_stride, int impl,
-                              double* out, double* trace, uint32_t trcap, hipStream_t s);
+                              double* out, double* trace, uint32_t trcap, hipStream_t s, bool plain = false);
 int scale_impl();  // SVO_SCALE_IMPL knob (0 auto)
 int64_t ref_sel_stride(int64_t max_slots);  // K2R scratch per pair (u32) for vectors of up to max_slots
 // K2V (align_refv.hip): the same selection with the vector in registers, vectors of <= refv_max_slots()
 int64_t refv_max_slots();
 void launch_scale_refv(const AlignArgs& a, int level, hipStream_t s);
 void launch_debug_robust_scale_v(const double* v, uint32_t M, uint32_t n, double* gseg, double* out, double* trace,
-                                 uint32_t trcap, hipStream_t s);
+                                 uint32_t trcap, hipStream_t s, bool plain);
 int align_max_half();  // largest patch half size the alignment kernels are instantiated for
 int align_feat_iters();                                 // feature groups per K1/K3 wave
 int align_win_dwords(int half);                         // window dwords per feature (win_stride / slots)

@@ -21,7 +21,7 @@ usage: python3 tools/check_vreg_fence.py <device assembly .s>
 import re
 import sys
 
-KERNELS = ("align_scale_refv_kernel", "debug_robust_scale_v_kernel")
+KERNELS = ("align_scale_refv_kernel", "debug_robust_scale_v_kernel", "plain_robust_scale_v_kernel")
 REG = re.compile(r"\bv\[?(\d+)(?::(\d+))?\]?")
 TAG = re.compile(r";@vfix\s+([\d,]+)")
 
