@@ -1217,8 +1217,15 @@ template <int kHalf, bool kWin>  // kWin: a window level (AlignArgs::win_levels)
 __global__ void __launch_bounds__(kLaneFeats, kHalf <= 2 ? 4 : 3) align_weights_kernel(AlignArgs a, int level) {
     using G = Win<kHalf>;
     constexpr int h = G::h, side = G::side, WB = G::WB, NW = G::WW;
-    __shared__ SolveShared ssh;
-    __shared__ double part[kLaneWaves][28];
+    // the wave partials and the LM step's workspace share their LDS (the step starts after the last read of the
+    // partials, two barriers later): ~0.9 KB per workgroup, so that up to three K3 workgroups fit beside a K2V
+    // workgroup whose waves 1-7 have ended (K2V leaves 3.4 KB of the CU's LDS unallocated)
+    __shared__ union {
+        SolveShared ssh;
+        double part[kLaneWaves][28];
+    } lds;
+    SolveShared& ssh = lds.ssh;
+    double (&part)[kLaneWaves][28] = lds.part;
     __shared__ uint32_t last_flag;
     SVO_TL_SCOPE(k13, kTlK3, level, a.pair_base);
     int pair, chunk;
