@@ -1233,7 +1233,15 @@ struct VSel {
             }
             if (wave == 0) {
                 uint32_t nw = 0;
+#if defined(SVO_K2V_PRIO)
+                // the last pass's one-wave rounds are the pair's critical path while other kernels' workgroups may
+                // share the CU (waves 1-7 retired): wave 0 issues first on its SIMD
+                if (retire) __builtin_amdgcn_s_setprio(3);
+#endif
                 wave_rounds(seg, sh.mbx + kOneWave, nw);
+#if defined(SVO_K2V_PRIO)
+                if (retire) __builtin_amdgcn_s_setprio(0);
+#endif
                 if (tid == 0) {
                     if (l - f <= 3) {  // std::__insertion_sort of the last <= 3
                         const uint32_t n = l - f;
