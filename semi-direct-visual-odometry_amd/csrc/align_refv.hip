@@ -81,7 +81,10 @@ struct Lay {
     // stage_wave0: waves 1..7 take rows wave - 1 + 7 i, i < R / 7, which reaches every row only for R a multiple of 7
     static_assert(!PRE || R % (kVW - 1) == 0, "stage_wave0 covers every row");
 };
-using LayA = Lay<RowsA, 98, 12288, true, SVO_ONEWAVE>;   // 50 176 slots: 88 register rows (v80..v255) + 10 LDS rows
+#ifndef SVO_ONEWAVE_A
+#define SVO_ONEWAVE_A SVO_ONEWAVE
+#endif
+using LayA = Lay<RowsA, 98, 12288, true, SVO_ONEWAVE_A>;   // 50 176 slots: 88 register rows (v80..v255) + 10 LDS rows
 using LayB = Lay<RowsB, 118, 4352, false, SVO_ONEWAVE>;  // 60 416 slots: 92 register rows (v72..v255) + 26 LDS rows
 // 65 536 slots (2621 features at patch 5): 96 register rows (v64..v255) + 32 LDS rows; the LDS rows leave a 1344-swap
 // mailbox (163 032 of the CU's 163 840 LDS bytes in all), so the large rounds exchange in chunks, each walking only its
@@ -1233,15 +1236,7 @@ struct VSel {
             }
             if (wave == 0) {
                 uint32_t nw = 0;
-#if defined(SVO_K2V_PRIO)
-                // the last pass's one-wave rounds are the pair's critical path while other kernels' workgroups may
-                // share the CU (waves 1-7 retired): wave 0 issues first on its SIMD
-                if (retire) __builtin_amdgcn_s_setprio(3);
-#endif
                 wave_rounds(seg, sh.mbx + kOneWave, nw);
-#if defined(SVO_K2V_PRIO)
-                if (retire) __builtin_amdgcn_s_setprio(0);
-#endif
                 if (tid == 0) {
                     if (l - f <= 3) {  // std::__insertion_sort of the last <= 3
                         const uint32_t n = l - f;

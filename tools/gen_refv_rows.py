@@ -47,7 +47,7 @@ import os
 
 LAYOUTS = (("RowsA", 80), ("RowsB", 72), ("RowsC", 64))
 # the one-wave rounds' quads (rows 0 .. 4 W1QUADS - 1 of wave 0: one-wave segments of up to 256 W1QUADS positions)
-W1QUADS = 8
+W1QUADS = int(os.environ.get("SVO_GEN_W1QUADS", "8"))
 # the quads' instruction-level parallelism form (cls4_ilp / exch_ilp): compares first, then independent per-row chains
 ILP = os.environ.get("SVO_GEN_ILP", "1") == "1"
 OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "semi-direct-visual-odometry_amd",
