@@ -116,3 +116,25 @@ def test_positions_read_only_and_point_construction_keeps_caches():
     g.frame = other
     assert fr.feature_arrays()[0] is not a[0] and other.feature_arrays()[0] is not b[0]
     assert _same([fr]) and _same([other])
+
+
+def test_point_copies_own_their_row():
+    """copy.copy / deepcopy / pickle of a Point allocate a row of their own (copying the row index would
+    alias one row between two Points and free it twice)."""
+    import copy
+    import pickle
+    p = svo_amd.Point([1.0, 2.0, 3.0])
+    p.type = svo_amd.PointType.GOOD
+    p.last_projected_kf_id = 7
+    p.succeeded_projection = 3
+    for q in (copy.copy(p), copy.deepcopy(p), pickle.loads(pickle.dumps(p))):
+        assert q._i != p._i
+        assert np.array_equal(q.position, p.position) and q.type == p.type
+        assert q.last_projected_kf_id == 7 and q.succeeded_projection == 3 and q.failed_projection == 0
+        q.position = [9.0, 9.0, 9.0]  # the copy's row is its own
+        assert np.array_equal(p.position, [1.0, 2.0, 3.0])
+    free0 = len(core._PT.free)
+    del q
+    import gc
+    gc.collect()
+    assert len(set(core._PT.free)) == len(core._PT.free) >= free0  # no row on the free list twice
