@@ -43,7 +43,7 @@ def main(path):
         v = groups[k]
         name, gx, gy, gz = k
         pairs = ""
-        if name.startswith("align_scale_ref") and wg[k]:
+        if "align_scale_ref" in name and wg[k]:
             pairs = gx // wg[k]
         w.writerow([name, gx, gy, gz, wg[k], pairs, len(v), round(statistics.median(v), 2), round(statistics.mean(v), 2),
                     round(pct(v, 0.1), 2), round(pct(v, 0.9), 2), round(min(v), 2), round(max(v), 2),
