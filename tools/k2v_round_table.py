@@ -4,14 +4,15 @@ For config-2 scenes (seeds 0x5EED0000 + i, 2000 features, patch 5, 5 levels) the
 vector (oracle.image_align_vectors); both passes of computeMedian / computeMAD (src/algorithm.cpp:834-865) are run
 through the numpy round model (tests/introselect_rounds.py, pinned to std::nth_element) and every round is tabulated:
 segment S, Ks (swaps), the cut, the kept side, the discarded side.  K2V runs a round as a block round while S exceeds
-its one-wave size (1024 positions, LayA), so the table splits rounds into block and one-wave rounds.
+its one-wave size, so the table splits rounds into block and one-wave rounds.  `--one-wave` sets that size: 1024 (the
+default) reproduces profiles/r06_k2v_round_table.json; the product layouts use 2048 since DESIGN 19.7.
 
 Item 3 (two pairs per CU on 4-byte keys): for the same vectors, how often distinct doubles share the top 32 bits of the
 order-preserving 64-bit key (the 4-byte key), and how often a round's pivot -- the value every comparison of the round
 is made against -- or the final vec[nth - 1] / vec[nth] shares its bucket with a distinct value (where a 4-byte key
 would decide a comparison differently from the reference's double `<`).
 
-usage: python3 tools/k2v_round_table.py [--scenes N] [--json out.json]
+usage: python3 tools/k2v_round_table.py [--scenes N] [--one-wave 1024|2048] [--json out.json]
 """
 import argparse
 import json
@@ -28,7 +29,6 @@ import oracle as O  # noqa: E402
 import svo_amd.synth as synth  # noqa: E402
 from introselect_rounds import DBL_MAX, rounds  # noqa: E402
 
-ONE_WAVE = 1024
 
 
 def key32(v):
@@ -106,22 +106,24 @@ def analyse(i):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", type=int, default=16)
+    ap.add_argument("--one-wave", type=int, default=1024)
     ap.add_argument("--json", default="")
     args = ap.parse_args()
+    one_wave = args.one_wave
     with ThreadPoolExecutor(min(8, os.cpu_count() or 1)) as ex:
         rows = [r for rs in ex.map(analyse, range(args.scenes)) for r in rs]
-    summary = {"scenes": args.scenes, "vectors": len(rows) // 2}
+    summary = {"scenes": args.scenes, "vectors": len(rows) // 2, "one_wave": one_wave}
     for P in (0, 1):
         blk, onew, lops, small_ks = [], [], [], []
         for r in rows:
             if r["pass"] != P:
                 continue
-            b = [x for x in r["rounds"] if x[0] > ONE_WAVE]
+            b = [x for x in r["rounds"] if x[0] > one_wave]
             blk.append(len(b))
             onew.append(len(r["rounds"]) - len(b))
             lops += [x for x in b if x[4] < 0.3 * x[0]]       # rounds that discard < 30 % of the segment
             small_ks += [x for x in b if x[1] <= 64]          # rounds whose exchange is <= 64 swaps
-        allb = [x for r in rows if r["pass"] == P for x in r["rounds"] if x[0] > ONE_WAVE]
+        allb = [x for r in rows if r["pass"] == P for x in r["rounds"] if x[0] > one_wave]
         summary[f"pass{P}"] = {
             "block_rounds_per_call_mean": round(float(np.mean(blk)), 2), "block_rounds_max": int(max(blk)),
             "one_wave_rounds_per_call_mean": round(float(np.mean(onew)), 2),
