@@ -24,7 +24,11 @@ v[np.repeat(rng.random(NS // 25) < 0.2, 25)] = DBL_MAX
 n = int((v < 1e300).sum())
 ctx = svo_amd.default_context()
 impl = int(sys.argv[1]) if len(sys.argv) > 1 else svo_amd.SCALE_K2R
-out = np.zeros(206)
+# SVO_PROBE_PLAIN=1: out_len 2, so K2V runs the product kernel (plain_robust_scale_v_kernel: product layouts, one-wave
+# size 2048, wave retirement) instead of the diagnostics kernel; only the result and the call time are reported, the
+# kernel's own duration comes from a kernel trace of this run.
+plain = bool(os.environ.get("SVO_PROBE_PLAIN"))
+out = np.zeros(2 if plain else 206)
 for _ in range(3):
     _capi.check(_capi.lib().svo_debug_robust_scale(ctx.handle, _capi.ptr(v), len(v), n, impl, _capi.ptr(out), len(out)))
 t0 = time.perf_counter()
@@ -36,7 +40,10 @@ d = np.abs(v - med_c)
 d[v >= DBL_MAX] = DBL_MAX
 mad_c = O.median(d, n, 0)
 match = out[0] == med_c and out[1] == mad_c
-print(f"med {out[0]!r} mad {out[1]!r}  oracle {med_c!r} {mad_c!r}  match {match}  call {dt * 1e6:.1f} us")
+print(f"med {out[0]!r} mad {out[1]!r}  oracle {med_c!r} {mad_c!r}  match {match}  call {dt * 1e6:.1f} us"
+      + ("  (product kernel)" if plain else ""))
+if plain:
+    sys.exit(0 if match else 3)
 if impl == svo_amd.SCALE_K2V:
     for p in range(2):
         cyc, nb, nl, hp, ch = out[2 + 5 * p: 7 + 5 * p]
