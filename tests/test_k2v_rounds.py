@@ -93,3 +93,7 @@ def test_k2v_every_round_matches_model(fam):
         else:
             assert out[1] == r
     assert ri >= 10 or ns < 1000
+    # the product kernel (2048-position one-wave rounds in LayA / LayB, waves 1-7 retiring) on the same
+    # vector: the same introselect, so the same median and MAD
+    pm, pd = svo_amd.debug_robust_scale(v, n, impl=svo_amd.SCALE_K2V)
+    assert (pm, pd) == (out[0], out[1]), ("product", pm, out[0], pd, out[1])

@@ -99,7 +99,8 @@ def test_debug_robust_scale_matches_nth_element(case, impl):
 def test_debug_robust_scale_k2v_extremes():
     """K2V at the capacity of each register layout (LayA 50 176 slots, LayB 60 416, LayC 65 536: every register row
     and LDS row in use), vectors whose first round needs a chunked exchange (Ks > the mailbox: reversed order; LayB's
-    4 352-slot mailbox chunks most of its first rounds), all-invisible tails, and n_valid far below the length."""
+    4 352-slot mailbox chunks most of its first rounds), all-invisible tails, and n_valid far below the length; each
+    through the diagnostics kernel and through the product kernel."""
     rng = np.random.default_rng(11)
     cases = []
     for cap in sorted({svo_amd.SCALE_K2V_LAYA_SLOTS, svo_amd.SCALE_K2V_LAYB_SLOTS, svo_amd.SCALE_K2V_MAX_SLOTS}):
@@ -121,6 +122,9 @@ def test_debug_robust_scale_k2v_extremes():
         med_c, mad_c = oracle_med_mad(v, n)
         assert med == med_c and mad == mad_c, (len(v), n, med, med_c, mad, mad_c, dg[:10])
         chunked.append(dg[4] + dg[9])  # block rounds whose exchange ran in mailbox chunks (both passes)
+        # the product kernel on the same vector (its layouts' one-wave size and wave retirement)
+        pm, pd = svo_amd.debug_robust_scale(v, n, impl=svo_amd.SCALE_K2V)
+        assert pm == med_c and pd == mad_c, ("product", len(v), n, pm, med_c, pd, mad_c)
     assert all(chunked[desc + i] >= 1 for i in range(3)), chunked  # the descending vectors exercise the chunked exchange
 
 
